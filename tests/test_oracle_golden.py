@@ -1,0 +1,104 @@
+"""Pin the CPU oracle (oracle/apm_oracle.py, oracle/gram.c) against golden vectors
+produced by the reference itself (tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+import apm_oracle as orc
+from conftest import golden
+
+
+def _gram_cases():
+    g = golden('gram')
+    keys = sorted({k.rsplit('_', 1)[0] for k in g.files if k.endswith('_thetas')})
+    return g, keys
+
+
+@pytest.mark.parametrize('impl', ['numpy', 'c'])
+def test_gram_matches_reference(impl):
+    g, keys = _gram_cases()
+    for key in keys:
+        kind = key.split('_')[0]
+        X = g[key + '_X']
+        for th, Kref in zip(g[key + '_thetas'], g[key + '_K']):
+            K = np.empty_like(Kref)
+            if impl == 'c':
+                orc.c_gram(kind, K, X, th, 1e-8)
+                # same op order, same libm exp -> bit-exact with the Cython build
+                np.testing.assert_array_equal(K, Kref)
+            else:
+                (orc.iso_se_kernel if kind == 'iso' else orc.ard_se_kernel)(K, X, th, 1e-8)
+                np.testing.assert_allclose(K, Kref, rtol=1e-14, atol=1e-300)
+
+
+def test_gram_extra_theta_ignored():
+    g = golden('gram')
+    K = np.empty((9, 9))
+    orc.c_gram('iso', K, g['extra_theta_X'], np.array([0.1, 0.2, 99.]), 1e-8)
+    np.testing.assert_array_equal(K, g['extra_theta_K'])
+
+
+def _cases():
+    g = golden('estimators')
+    for ci in range(int(g['n_cases'])):
+        pre = 'c{0}_'.format(ci)
+        yield ci, {k[len(pre):]: g[k] for k in g.files if k.startswith(pre)}
+
+
+def test_laplace_matches_reference():
+    for ci, c in _cases():
+        f, C, lml, nops = orc.laplace_approximation(c['K'], c['y'], True, True)
+        np.testing.assert_allclose(f, c['lap_f'], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(C, c['lap_C'], rtol=1e-9, atol=1e-12)
+        assert abs(lml - float(c['lap_lml'])) < 1e-9 * max(1., abs(float(c['lap_lml'])))
+        assert nops == int(c['lap_nops_cov_lml'])
+        f2, nops2 = orc.laplace_approximation(c['K'], c['y'], False, False)
+        assert nops2 == int(c['lap_nops_plain'])
+
+
+def test_is_estimator_matches_reference():
+    for ci, c in _cases():
+        kf = orc.make_kernel_func(str(c['kind']), 1e-8)
+        v1, cache, ops = orc.is_estimate(c['X'], c['y'], kf, c['ns1'], c['theta'])
+        assert abs(v1 - float(c['is_logf1'])) < 1e-8 * max(1., abs(v1)), ci
+        assert ops == int(c['is_ops'])
+        v2, _, ops2 = orc.is_estimate(c['X'], c['y'], kf, c['ns2'], None, cache)
+        assert abs(v2 - float(c['is_logf2'])) < 1e-8 * max(1., abs(v2)), ci
+        assert ops2 == 0
+        np.testing.assert_allclose(cache[2], c['f_post'], rtol=1e-10, atol=1e-12)
+
+
+def test_priormc_and_laplace_estimators_match_reference():
+    for ci, c in _cases():
+        kf = orc.make_kernel_func(str(c['kind']), 1e-8)
+        p1, Kc, ops = orc.priormc_estimate(c['X'], c['y'], kf, c['ns1'], c['theta'])
+        assert abs(p1 - float(c['pmc_logf1'])) < 1e-9 * max(1., abs(p1))
+        p2, _, _ = orc.priormc_estimate(c['X'], c['y'], kf, c['ns2'], None, Kc)
+        assert abs(p2 - float(c['pmc_logf2'])) < 1e-9 * max(1., abs(p2))
+        lml, ops = orc.laplace_estimate(c['X'], c['y'], kf, c['theta'])
+        assert abs(lml - float(c['lapest_lml'])) < 1e-9 * max(1., abs(lml))
+        assert ops == int(c['lapest_ops'])
+
+
+def test_reformulated_is_equals_reference_form():
+    """The GPU computes the algebraically identical form of estimators.py:221-241
+    (DESIGN.md §3); pin that identity on the reference's own outputs."""
+    for ci, c in _cases():
+        st = orc.theta_state_reformulated(c['K'], c['y'])
+        for ns, key in ((c['ns1'], 'is_logf1'), (c['ns2'], 'is_logf2')):
+            v = orc.is_estimate_reformulated(c['y'], st, ns)
+            ref = float(c[key])
+            assert abs(v - ref) < 1e-7 * max(1., abs(ref)), (ci, v, ref)
+
+
+def test_laplace_max_iters_error():
+    e = golden('errors')
+    with pytest.raises(orc.MaximumIterationsExceededError) as ei:
+        orc.laplace_approximation(e['K'], e['y'], max_iters=1)
+    assert str(ei.value) == str(e['laplace_maxiter_msg'])
+
+
+def test_utils_match_reference():
+    u = golden('utils')
+    np.testing.assert_allclose(orc.log_gamma_log_pdf(u['x'], 1.1, 0.1), u['lgl'], rtol=1e-14)
+    Xn, mn, sd = orc.normalise_inputs(u['Xraw'])
+    np.testing.assert_allclose(Xn, u['Xn'], rtol=1e-14)
