@@ -1,0 +1,107 @@
+// Internal launcher interface between the kernel translation units and capi.cpp.
+// Nothing here is part of the public C-ABI (include/apm.h).
+#pragma once
+#include "apm_common.h"
+
+// A batched fp64 matrix: chain b's element (r, c) lives at base[b*cstride + r*ld + c].
+struct MatB {
+    double* base;
+    int64_t ld;
+    int64_t cstride;
+};
+
+// Per-chain liveness: a kernel does work for chain b iff active[b] != 0 && status[b] == 0.
+struct Live {
+    const int* active;
+    int* status;
+};
+
+// ---- chol.hip -------------------------------------------------------------------------------
+// Blocked right-looking Cholesky building blocks over TB x TB tiles (lower triangle).
+// diag:   factor tile (k,k) in place, write its inverse to Dinv[b][k] and sum(log diag) to
+//         ldet[b][k]; a non-positive pivot sets status[b] = fail_code.
+// panel:  tiles (i,k), i in [i0, R):  A_ik <- A_ik * inv(L_kk)^T     (f64 MFMA)
+// update: tiles (i,j), i in [i0, R), k < j <= min(i, Cb-1):  A_ij -= A_ik A_jk^T  (f64 MFMA)
+void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
+                      Live live, int fail_code, int nchains, hipStream_t s);
+void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
+                       Live live, int nchains, hipStream_t s);
+void launch_chol_update(MatB A, int k, int i0, int R, int Cb, Live live, int nchains,
+                        hipStream_t s);
+// one step (block J) of the backward solve L^T z = r, r stored in row `rrow` of A (in place),
+// z written to z[b*zstride + ...]
+void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,
+                         double* z, int64_t zstride, Live live, int nchains, hipStream_t s);
+// test hook: C(64x64) = A(64x64) * B(64x64)^T through the MFMA tile path
+void launch_tile_nt_test(const double* A, const double* B, double* C, hipStream_t s);
+
+// ---- gram.hip -------------------------------------------------------------------------------
+// K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
+// kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
+void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
+                 int64_t tstride, int kind, double eps, int np, Live live, int nchains,
+                 hipStream_t s);
+
+// ---- newton.hip -----------------------------------------------------------------------------
+struct NewtonVecs {     // all per chain, stride vstride (>= np)
+    double* f;          // current mode estimate
+    double* fnew;
+    double* W;          // W_diag
+    double* Ws;         // W_diag^1/2
+    double* b;          // W f + grad
+    double* Kb;         // K b, later reused
+    double* a;          // b - W^1/2 z
+    double* z;          // TRSV result
+    int64_t vstride;
+};
+void launch_newton_prep(NewtonVecs v, const double* y, int n, int np, Live live, int nchains,
+                        hipStream_t s);
+void launch_gemv(MatB M, const double* x, int64_t xstride, double* out, int64_t ostride, int np,
+                 Live live, int nchains, hipStream_t s);
+void launch_form_B(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains, hipStream_t s);
+void launch_newton_update(NewtonVecs v, int np, Live live, int nchains, hipStream_t s);
+void launch_newton_check(NewtonVecs v, int n, int np, double tol, int* active, const int* status,
+                         int* n_iter, int nchains, hipStream_t s);
+void launch_copy_lower(MatB src, MatB dst, int np, Live live, int nchains, hipStream_t s);
+void launch_form_aug(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains,
+                     hipStream_t s);
+// per chain: out[b] = -0.5 a.f + sum_n log_ndtr(y f) - 0.5*sum(ldet[0..nb))*2
+void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet,
+                        int64_t lstride, int nb, double* out, Live live, int nchains,
+                        hipStream_t s);
+
+// cache slot: fp32 factor with an extra TB-row block (row np holds g^T), plus vectors
+struct SlotSet {
+    float* L;           // (np + TB) x np, ld = np
+    float* fpost;       // np
+    float* W;           // np
+    double* fpost64;    // np
+    double* cst;        // 1 per slot: -1/2|g|^2 - 1/2 log|B|  (0 for PriorMC)
+    int64_t lstride, vstride;
+};
+// write slot slots[b] from the factored work matrix. mode 0 = IS (C_chol at offset (np,np),
+// g in row 2np), mode 1 = PriorMC (K_chol at (0,0), g = 0)
+void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
+                       SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
+                       int nchains, hipStream_t s);
+
+// ---- ugemm.hip ------------------------------------------------------------------------------
+struct UPool {
+    float* base;        // each buffer: np x sp fp32, ld = sp, zero padded
+    int64_t stride;
+    int sp;
+};
+void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int64_t ubuf,
+                      hipStream_t s);
+void launch_u_normal(UPool P, const int64_t* ubufs, const uint64_t* seeds,
+                     const uint64_t* counters, int n, int S, int nchains, hipStream_t s);
+void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64_t* b,
+                      const double* ca, const double* cb, int n, int S, int nchains,
+                      hipStream_t s);
+// partial[b][i][s] = sum over rows of row-block i of t(n,s) (i < nb), partial[b][nb][s] = g^T u_s
+void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
+                  const double* y, int n, int np, double* partial, int64_t pstride,
+                  const int* status, int nchains, hipStream_t s);
+void launch_lme(const double* partial, int64_t pstride, int nb, int S, int sp, SlotSet Sl,
+                const int64_t* slots, double* out, const int* status, int nchains,
+                hipStream_t s);

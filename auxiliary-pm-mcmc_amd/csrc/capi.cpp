@@ -1,0 +1,797 @@
+// C-ABI (include/apm.h) and host orchestration of the theta-call / u-call pipelines.
+//
+// theta-call (ApproxPosteriorIS, gpdemo/estimators.py:203-241), per batch of chains, one stream:
+//   Gram -> Newton loop { prep, K b, form B|rhs, chol(B) (+ forward solve), L^T solve, a, K a,
+//   check } -> augmented chol [[B,.],[K W^1/2, K],[0, f_post^T]] -> slot -> L.U + probit -> LME
+// The only host syncs are one per Newton iteration (convergence flags) and one at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/apm.h"
+#include "apm_internal.h"
+
+#define APM_VERSION 1
+
+static thread_local std::string g_err;
+
+struct ProfRec {
+    hipEvent_t a, b;
+    int kind;
+    double work;
+};
+
+struct apm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
+    int max_batch = 0, n_slots = 0, n_ubufs = 0;
+    double eps = 1e-8, tol = 1e-4;
+    int64_t max_iters = 1000;
+    std::string err;
+    // device data
+    double *X = nullptr, *y = nullptr, *theta = nullptr;
+    MatB K{}, A{};
+    double *Dinv = nullptr, *ldet = nullptr, *out = nullptr, *partial = nullptr;
+    int64_t dstride = 0, lstride = 0, pstride = 0;
+    NewtonVecs v{};
+    double* vecbase = nullptr;
+    int *active = nullptr, *status = nullptr, *n_iter = nullptr;
+    int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;
+    double *d_ca = nullptr, *d_cb = nullptr;
+    uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
+    double* U64 = nullptr;
+    SlotSet Sl{};
+    UPool Up{};
+    std::vector<void*> allocs;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> evpool;
+    size_t evnext = 0;
+    std::vector<ProfRec> recs;
+};
+
+namespace {
+
+struct HipError {
+    std::string msg;
+};
+
+#define HIPC(x)                                                                              \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess)                                                                \
+            throw HipError{std::string(#x) + ": " + hipGetErrorString(e_)};                  \
+    } while (0)
+
+template <class T>
+T* dalloc(apm_ctx* c, size_t count) {
+    void* p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e != hipSuccess)
+        throw HipError{"hipMalloc(" + std::to_string(count * sizeof(T)) +
+                       " bytes): " + hipGetErrorString(e)};
+    c->allocs.push_back(p);
+    return static_cast<T*>(p);
+}
+
+int fail(apm_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    g_err = m;
+    return code;
+}
+
+void check_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw HipError{std::string("kernel launch: ") + hipGetErrorString(e)};
+}
+
+// ------------------------------------------------------------------------------- profiling
+hipEvent_t next_event(apm_ctx* c) {
+    if (c->evnext == c->evpool.size()) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        c->evpool.push_back(e);
+    }
+    return c->evpool[c->evnext++];
+}
+
+struct ProfScope {
+    apm_ctx* c;
+    int kind;
+    double work;
+    hipEvent_t a{}, b{};
+    ProfScope(apm_ctx* c_, int k, double w) : c(c_), kind(k), work(w) {
+        if (c->prof) {
+            a = next_event(c);
+            b = next_event(c);
+            HIPC(hipEventRecord(a, c->stream));
+        }
+    }
+    ~ProfScope() {
+        if (c->prof && hipEventRecord(b, c->stream) == hipSuccess)
+            c->recs.push_back(ProfRec{a, b, kind, work});
+    }
+};
+
+// ------------------------------------------------------------------------------- building blocks
+Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
+
+void chol_range(apm_ctx* c, int k0, int k1, int R, int Cb, int fail_code, int count,
+                bool factor_diag = true, int row_start = 0) {
+    const Live lv = live_of(c);
+    for (int k = k0; k < k1; ++k) {
+        const int i0 = std::max(k + 1, row_start);
+        if (factor_diag) {
+            launch_chol_diag(c->A, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
+                             count, c->stream);
+            check_launch();
+        }
+        launch_chol_panel(c->A, k, i0, R, c->Dinv, c->dstride, lv, count, c->stream);
+        check_launch();
+        // algorithmic flops of this trailing update: off-diagonal tiles 2*64^3, diagonal tiles
+        // 64*65*64 (lower half), summed over the tiles actually updated
+        double flops = 0.0;
+        if (c->prof) {
+            for (int i = i0; i < R; ++i) {
+                const int jmax = std::min(i, Cb - 1);
+                for (int j = k + 1; j <= jmax; ++j)
+                    flops += (i == j) ? 64.0 * 65.0 * 64.0 : 2.0 * 64.0 * 64.0 * 64.0;
+            }
+            flops *= count;
+        }
+        ProfScope ps(c, APM_PROF_CHOL_UPDATE, flops);
+        launch_chol_update(c->A, k, i0, R, Cb, lv, count, c->stream);
+        check_launch();
+    }
+}
+
+void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
+
+void u_eval_device(apm_ctx* c, int count) {
+    {
+        ProfScope ps(c, APM_PROF_UGEMM, (double)c->n * (c->n + 1) * c->S * count);
+        launch_ugemm(c->Sl, c->d_slots, c->Up, c->d_ubufs, c->y, c->n, c->np, c->partial,
+                     c->pstride, c->status, count, c->stream);
+        check_launch();
+    }
+    launch_lme(c->partial, c->pstride, c->nb, c->S, c->sp, c->Sl, c->d_slots, c->out, c->status,
+               count, c->stream);
+    check_launch();
+}
+
+// Newton loop of laplace_approximation over the live chains; returns host n_iter per chain.
+void newton(apm_ctx* c, int count, std::vector<int>& st_h) {
+    const Live lv = live_of(c);
+    HIPC(hipMemsetAsync(c->v.f, 0, sizeof(double) * c->v.vstride * count, c->stream));
+    std::vector<int> act(count, 1);  // max_iters == 0: every chain is unconverged
+    const int64_t rrow = c->np;  // Newton rhs row (extra row block below B)
+    int64_t it = 0;
+    for (; it < c->max_iters; ++it) {
+        launch_newton_prep(c->v, c->y, c->n, c->np, lv, count, c->stream);
+        check_launch();
+        launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
+                    c->stream);
+        check_launch();
+        launch_form_B(c->K, c->A, c->v, c->np, lv, count, c->stream);
+        check_launch();
+        chol_range(c, 0, c->nb, c->nb + 1, c->nb, APM_STATUS_CHOL_B, count);
+        for (int J = c->nb - 1; J >= 0; --J) {
+            launch_trsv_lt_step(c->A, J, rrow, c->Dinv, c->dstride, c->v.z, c->v.vstride, lv,
+                                count, c->stream);
+            check_launch();
+        }
+        launch_newton_update(c->v, c->np, lv, count, c->stream);
+        check_launch();
+        launch_gemv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->np, lv, count,
+                    c->stream);
+        check_launch();
+        launch_newton_check(c->v, c->n, c->np, c->tol, c->active, c->status, c->n_iter, count,
+                            c->stream);
+        check_launch();
+        HIPC(hipMemcpyAsync(act.data(), c->active, sizeof(int) * count, hipMemcpyDeviceToHost,
+                            c->stream));
+        HIPC(hipMemcpyAsync(st_h.data(), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
+                            c->stream));
+        sync(c);
+        bool any = false;
+        for (int b = 0; b < count; ++b) any |= (act[b] != 0 && st_h[b] == 0);
+        if (!any) break;
+    }
+    bool changed = false;
+    for (int b = 0; b < count; ++b)
+        if (act[b] != 0 && st_h[b] == 0) {
+            st_h[b] = APM_STATUS_MAXITER;
+            changed = true;
+        }
+    if (changed)
+        HIPC(hipMemcpyAsync(c->status, st_h.data(), sizeof(int) * count, hipMemcpyHostToDevice,
+                            c->stream));
+}
+
+// Posterior-covariance stage on the augmented matrix. With `factor_C` false the
+// bottom-right block is left holding C = K - V^T V (used by apm_laplace's calc_cov).
+void augmented(apm_ctx* c, int count, bool factor_C) {
+    const Live lv = live_of(c);
+    HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
+    launch_form_aug(c->K, c->A, c->v, c->np, lv, count, c->stream);
+    check_launch();
+    const int nb = c->nb, R = 2 * nb + 1, Cb = 2 * nb;
+    // top-left L (and its diagonal-block inverses) are the last Newton factorisation
+    chol_range(c, 0, nb, R, Cb, APM_STATUS_CHOL_B, count, /*factor_diag=*/false, /*rows>=*/nb);
+    if (factor_C) chol_range(c, nb, 2 * nb, R, Cb, APM_STATUS_CHOL_C, count);
+}
+
+void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf, int* status,
+                     int64_t* nops) {
+    const Live lv = live_of(c);
+    HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
+    HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
+    HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
+    if (gram) {
+        ProfScope ps(c, APM_PROF_GRAM,
+                     8.0 * ((double)c->n * c->d + (double)c->n * c->n) * count + 8.0 * c->P);
+        launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
+                    count, c->stream);
+        check_launch();
+    }
+    std::vector<int> st_h(count, 0), it_h(count, 0);
+    if (est == APM_EST_PRIORMC) {
+        launch_copy_lower(c->K, c->A, c->np, lv, count, c->stream);
+        check_launch();
+        chol_range(c, 0, c->nb, c->nb, c->nb, APM_STATUS_CHOL_K, count);
+        launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 1, c->n,
+                          c->np, lv, count, c->stream);
+        check_launch();
+        u_eval_device(c, count);
+    } else {
+        newton(c, count, st_h);
+        if (est == APM_EST_LAPLACE) {
+            launch_laplace_lml(c->v, c->y, c->n, c->ldet, c->lstride, c->nb, c->out, lv, count,
+                               c->stream);
+            check_launch();
+        } else {
+            augmented(c, count, true);
+            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 0, c->n,
+                              c->np, lv, count, c->stream);
+            check_launch();
+            u_eval_device(c, count);
+        }
+    }
+    HIPC(hipMemcpyAsync(out_logf, c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
+                        c->stream));
+    HIPC(hipMemcpyAsync(st_h.data(), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
+                        c->stream));
+    HIPC(hipMemcpyAsync(it_h.data(), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
+                        c->stream));
+    sync(c);
+    for (int b = 0; b < count; ++b) {
+        status[b] = st_h[b];
+        if (nops) {
+            if (est == APM_EST_PRIORMC) nops[b] = 1;                   // estimators.py:322
+            else if (est == APM_EST_LAPLACE) nops[b] = it_h[b];        // lpa.py:441-443 (i)
+            else nops[b] = (int64_t)it_h[b] + 1 + 2;                   // estimators.py:217
+        }
+    }
+}
+
+bool check_idx(apm_ctx* c, int64_t count, const int64_t* idx, int64_t lim, const char* what) {
+    for (int64_t i = 0; i < count; ++i)
+        if (idx[i] < 0 || idx[i] >= lim) {
+            fail(c, APM_E_INVALID, std::string(what) + " index out of range");
+            return false;
+        }
+    return true;
+}
+
+void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int64_t d,
+              int64_t ldx, const double* y, double eps, int64_t S, int64_t max_batch,
+              int64_t n_slots, int64_t n_ubufs) {
+    c->device = device;
+    HIPC(hipSetDevice(device));
+    HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->kind = kind;
+    c->n = (int)n;
+    c->d = (int)d;
+    c->np = (int)((n + 63) / 64 * 64);
+    c->nb = c->np / 64;
+    c->P = kind == APM_KERNEL_ISO ? 2 : (kind == APM_KERNEL_ARD ? (int)d + 1 : 0);
+    c->S = (int)S;
+    c->sp = (int)((S + 63) / 64 * 64);
+    c->max_batch = (int)max_batch;
+    c->n_slots = (int)n_slots;
+    c->n_ubufs = (int)n_ubufs;
+    c->eps = eps;
+    const int64_t np = c->np, B = max_batch;
+    if (kind != APM_KERNEL_PRECOMPUTED && d > 0) {
+        c->X = dalloc<double>(c, n * d);
+        std::vector<double> Xc((size_t)(n * d));
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t k = 0; k < d; ++k) Xc[i * d + k] = X[i * ldx + k];
+        HIPC(hipMemcpy(c->X, Xc.data(), sizeof(double) * n * d, hipMemcpyHostToDevice));
+    }
+    c->y = dalloc<double>(c, np);
+    std::vector<double> yp((size_t)np, 0.0);
+    if (y)
+        for (int64_t i = 0; i < n; ++i) yp[i] = y[i];
+    HIPC(hipMemcpy(c->y, yp.data(), sizeof(double) * np, hipMemcpyHostToDevice));
+    c->theta = dalloc<double>(c, B * std::max(c->P, 1));
+    c->K = MatB{dalloc<double>(c, B * np * np), np, np * np};
+    const int64_t arows = 2 * np + 64, acols = 2 * np;
+    c->A = MatB{dalloc<double>(c, B * arows * acols), acols, arows * acols};
+    c->dstride = 2 * c->nb * 4096;
+    c->Dinv = dalloc<double>(c, B * c->dstride);
+    c->lstride = 2 * c->nb;
+    c->ldet = dalloc<double>(c, B * c->lstride);
+    c->out = dalloc<double>(c, B);
+    c->pstride = (int64_t)(c->nb + 1) * c->sp;
+    c->partial = dalloc<double>(c, B * c->pstride);
+    const int64_t vs = np;
+    c->vecbase = dalloc<double>(c, 8 * B * vs);
+    c->v = NewtonVecs{c->vecbase,          c->vecbase + 1 * B * vs, c->vecbase + 2 * B * vs,
+                      c->vecbase + 3 * B * vs, c->vecbase + 4 * B * vs, c->vecbase + 5 * B * vs,
+                      c->vecbase + 6 * B * vs, c->vecbase + 7 * B * vs, vs};
+    HIPC(hipMemset(c->vecbase, 0, sizeof(double) * 8 * B * vs));
+    c->active = dalloc<int>(c, B);
+    c->status = dalloc<int>(c, B);
+    c->n_iter = dalloc<int>(c, B);
+    c->d_slots = dalloc<int64_t>(c, B);
+    c->d_ubufs = dalloc<int64_t>(c, B);
+    c->d_i3 = dalloc<int64_t>(c, 3 * B);
+    c->d_ca = dalloc<double>(c, B);
+    c->d_cb = dalloc<double>(c, B);
+    c->d_seeds = dalloc<uint64_t>(c, B);
+    c->d_ctrs = dalloc<uint64_t>(c, B);
+    c->U64 = dalloc<double>(c, n * S);
+    const int64_t Lsz = (np + 64) * np;
+    c->Sl = SlotSet{dalloc<float>(c, n_slots * Lsz), dalloc<float>(c, n_slots * np),
+                    dalloc<float>(c, n_slots * np), dalloc<double>(c, n_slots * np),
+                    dalloc<double>(c, n_slots), Lsz, np};
+    HIPC(hipMemset(c->Sl.cst, 0, sizeof(double) * n_slots));
+    c->Up = UPool{dalloc<float>(c, n_ubufs * np * c->sp), np * c->sp, c->sp};
+    HIPC(hipMemset(c->Up.base, 0, sizeof(float) * n_ubufs * np * c->sp));
+}
+
+void free_ctx(apm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void* p : c->allocs) (void)hipFree(p);
+    for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// stand-alone calls reuse one context per (device, n, kind) shape
+std::mutex g_mu;
+std::map<std::tuple<int, int64_t, int64_t, int>, apm_ctx*> g_cache;
+
+}  // namespace
+
+// =============================================================================== C-ABI
+extern "C" {
+
+int apm_version(void) { return APM_VERSION; }
+
+int apm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* apm_global_error(void) { return g_err.c_str(); }
+
+apm_ctx* apm_create(int device, int kernel_kind, const double* X, int64_t n, int64_t d,
+                    int64_t ldx, const double* y, double epsilon, int64_t n_imp,
+                    int64_t max_batch, int64_t n_slots, int64_t n_ubufs) {
+    if (n <= 0 || d < 0 || n_imp <= 0 || max_batch <= 0 || n_slots <= 0 || n_ubufs <= 0 ||
+        kernel_kind < 0 || kernel_kind > 2 || (kernel_kind != APM_KERNEL_PRECOMPUTED && !X) ||
+        n_imp > 1 << 20) {
+        g_err = "apm_create: invalid arguments";
+        return nullptr;
+    }
+    apm_ctx* c = new apm_ctx();
+    try {
+        init_ctx(c, device, kernel_kind, X, n, d, ldx, y, epsilon, n_imp, max_batch, n_slots,
+                 n_ubufs);
+    } catch (const HipError& e) {
+        g_err = "apm_create: " + e.msg;
+        free_ctx(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void apm_destroy(apm_ctx* ctx) { free_ctx(ctx); }
+
+const char* apm_last_error(const apm_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int64_t apm_padded_n(const apm_ctx* ctx) { return ctx ? ctx->np : -1; }
+
+int64_t apm_theta_len(const apm_ctx* ctx) { return ctx ? ctx->P : -1; }
+
+int apm_set_newton(apm_ctx* ctx, double diff_f_tol, int64_t max_iters) {
+    if (!ctx || max_iters < 0) return fail(ctx, APM_E_INVALID, "apm_set_newton: bad arguments");
+    ctx->tol = diff_f_tol;
+    ctx->max_iters = max_iters;
+    return APM_SUCCESS;
+}
+
+void* apm_stream(apm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int apm_u_upload(apm_ctx* c, int64_t ubuf, const double* U, int64_t ldu) {
+    if (!c || !U || ubuf < 0 || ubuf >= c->n_ubufs || ldu < c->S)
+        return fail(c, APM_E_INVALID, "apm_u_upload: bad arguments");
+    try {
+        HIPC(hipSetDevice(c->device));
+        HIPC(hipMemcpy2DAsync(c->U64, sizeof(double) * c->S, U, sizeof(double) * ldu,
+                              sizeof(double) * c->S, c->n, hipMemcpyHostToDevice, c->stream));
+        launch_u_convert(c->U64, c->S, c->n, c->S, c->Up, ubuf, c->stream);
+        check_launch();
+        sync(c);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_u_download(apm_ctx* c, int64_t ubuf, double* U, int64_t ldu) {
+    if (!c || !U || ubuf < 0 || ubuf >= c->n_ubufs || ldu < c->S)
+        return fail(c, APM_E_INVALID, "apm_u_download: bad arguments");
+    try {
+        HIPC(hipSetDevice(c->device));
+        std::vector<float> h((size_t)c->np * c->sp);
+        HIPC(hipMemcpyAsync(h.data(), c->Up.base + ubuf * c->Up.stride, sizeof(float) * h.size(),
+                            hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        for (int i = 0; i < c->n; ++i)
+            for (int s = 0; s < c->S; ++s) U[(int64_t)i * ldu + s] = h[(size_t)i * c->sp + s];
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_u_normal(apm_ctx* c, int64_t count, const int64_t* ubufs, const uint64_t* seeds,
+                 const uint64_t* counters) {
+    if (!c || count <= 0 || count > c->max_batch || !ubufs || !seeds || !counters)
+        return fail(c, APM_E_INVALID, "apm_u_normal: bad arguments");
+    if (!check_idx(c, count, ubufs, c->n_ubufs, "ubuf")) return APM_E_INVALID;
+    try {
+        HIPC(hipSetDevice(c->device));
+        HIPC(hipMemcpyAsync(c->d_i3, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+        HIPC(hipMemcpyAsync(c->d_seeds, seeds, sizeof(uint64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+        HIPC(hipMemcpyAsync(c->d_ctrs, counters, sizeof(uint64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+        launch_u_normal(c->Up, c->d_i3, c->d_seeds, c->d_ctrs, c->n, c->S, (int)count,
+                        c->stream);
+        check_launch();
+        sync(c);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_u_combine(apm_ctx* c, int64_t count, const int64_t* dst, const int64_t* a,
+                  const int64_t* b, const double* ca, const double* cb) {
+    if (!c || count <= 0 || count > c->max_batch || !dst || !a || !b || !ca || !cb)
+        return fail(c, APM_E_INVALID, "apm_u_combine: bad arguments");
+    if (!check_idx(c, count, dst, c->n_ubufs, "dst") || !check_idx(c, count, a, c->n_ubufs, "a") ||
+        !check_idx(c, count, b, c->n_ubufs, "b"))
+        return APM_E_INVALID;
+    try {
+        HIPC(hipSetDevice(c->device));
+        HIPC(hipMemcpyAsync(c->d_i3, dst, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_i3 + c->max_batch, a, sizeof(int64_t) * count,
+                            hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_i3 + 2 * c->max_batch, b, sizeof(int64_t) * count,
+                            hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_ca, ca, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_cb, cb, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+        launch_u_combine(c->Up, c->d_i3, c->d_i3 + c->max_batch, c->d_i3 + 2 * c->max_batch,
+                         c->d_ca, c->d_cb, c->n, c->S, (int)count, c->stream);
+        check_launch();
+        sync(c);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int64_t ldt,
+                   const int64_t* ubufs, const int64_t* slots, double* out_logf, int* status,
+                   int64_t* nops) {
+    if (!c || count <= 0 || count > c->max_batch || !thetas || !out_logf || !status ||
+        est < 0 || est > 2 || c->kind == APM_KERNEL_PRECOMPUTED || ldt < c->P)
+        return fail(c, APM_E_INVALID, "apm_theta_eval: bad arguments");
+    if (est != APM_EST_LAPLACE) {
+        if (!ubufs || !slots) return fail(c, APM_E_INVALID, "apm_theta_eval: ubufs/slots required");
+        if (!check_idx(c, count, slots, c->n_slots, "slot") ||
+            !check_idx(c, count, ubufs, c->n_ubufs, "ubuf"))
+            return APM_E_INVALID;
+    }
+    try {
+        HIPC(hipSetDevice(c->device));
+        std::vector<double> th((size_t)count * c->P);
+        for (int64_t b = 0; b < count; ++b)
+            for (int p = 0; p < c->P; ++p) th[b * c->P + p] = thetas[b * ldt + p];
+        HIPC(hipMemcpyAsync(c->theta, th.data(), sizeof(double) * th.size(), hipMemcpyHostToDevice,
+                            c->stream));
+        if (est != APM_EST_LAPLACE) {
+            HIPC(hipMemcpyAsync(c->d_slots, slots, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                                c->stream));
+            HIPC(hipMemcpyAsync(c->d_ubufs, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                                c->stream));
+        }
+        theta_eval_impl(c, est, (int)count, true, out_logf, status, nops);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t ubuf,
+                     int64_t slot, double* out_logf, int* status, int64_t* nops) {
+    if (!c || !K || ldk < c->n || !out_logf || !status || est < 0 || est > 2)
+        return fail(c, APM_E_INVALID, "apm_theta_eval_K: bad arguments");
+    if (est != APM_EST_LAPLACE &&
+        (slot < 0 || slot >= c->n_slots || ubuf < 0 || ubuf >= c->n_ubufs))
+        return fail(c, APM_E_INVALID, "apm_theta_eval_K: slot/ubuf out of range");
+    try {
+        HIPC(hipSetDevice(c->device));
+        // identity-padded copy of K into chain 0's K
+        std::vector<double> Kp((size_t)c->np * c->np, 0.0);
+        for (int i = 0; i < c->np; ++i)
+            for (int j = 0; j < c->np; ++j)
+                Kp[(size_t)i * c->np + j] =
+                    (i < c->n && j < c->n) ? K[(int64_t)i * ldk + j] : (i == j ? 1.0 : 0.0);
+        HIPC(hipMemcpyAsync(c->K.base, Kp.data(), sizeof(double) * Kp.size(),
+                            hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_slots, &slot, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->d_ubufs, &ubuf, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        theta_eval_impl(c, est, 1, false, out_logf, status, nops);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* ubufs,
+               double* out_logf, int* status) {
+    if (!c || count <= 0 || count > c->max_batch || !slots || !ubufs || !out_logf || !status)
+        return fail(c, APM_E_INVALID, "apm_u_eval: bad arguments");
+    if (!check_idx(c, count, slots, c->n_slots, "slot") ||
+        !check_idx(c, count, ubufs, c->n_ubufs, "ubuf"))
+        return APM_E_INVALID;
+    try {
+        HIPC(hipSetDevice(c->device));
+        HIPC(hipMemcpyAsync(c->d_slots, slots, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+        HIPC(hipMemcpyAsync(c->d_ubufs, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+        HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
+        u_eval_device(c, (int)count);
+        HIPC(hipMemcpyAsync(out_logf, c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
+                            c->stream));
+        HIPC(hipMemcpyAsync(status, c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
+                            c->stream));
+        sync(c);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_slot_read(apm_ctx* c, int64_t slot, double* L, int64_t ldl, double* f_post, double* g,
+                  double* cst) {
+    if (!c || slot < 0 || slot >= c->n_slots) return fail(c, APM_E_INVALID, "apm_slot_read: bad slot");
+    try {
+        HIPC(hipSetDevice(c->device));
+        const int64_t np = c->np;
+        if (L || g) {
+            std::vector<float> h((size_t)((np + 64) * np));
+            HIPC(hipMemcpyAsync(h.data(), c->Sl.L + slot * c->Sl.lstride, sizeof(float) * h.size(),
+                                hipMemcpyDeviceToHost, c->stream));
+            sync(c);
+            if (L)
+                for (int i = 0; i < c->n; ++i)
+                    for (int j = 0; j < c->n; ++j) L[(int64_t)i * ldl + j] = h[(size_t)i * np + j];
+            if (g)
+                for (int j = 0; j < c->n; ++j) g[j] = h[(size_t)np * np + j];
+        }
+        if (f_post) {
+            HIPC(hipMemcpyAsync(f_post, c->Sl.fpost64 + slot * c->Sl.vstride, sizeof(double) * c->n,
+                                hipMemcpyDeviceToHost, c->stream));
+        }
+        if (cst)
+            HIPC(hipMemcpyAsync(cst, c->Sl.cst + slot, sizeof(double), hipMemcpyDeviceToHost,
+                                c->stream));
+        sync(c);
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_gram(int device, int kind, const double* X, int64_t n, int64_t d, int64_t ldx,
+             const double* theta, int64_t n_theta, double eps, double* K, int64_t ldk) {
+    if (n <= 0 || d <= 0 || !X || !theta || !K || ldk < n || ldx < d ||
+        (kind != APM_KERNEL_ISO && kind != APM_KERNEL_ARD))
+        return fail(nullptr, APM_E_INVALID, "apm_gram: bad arguments");
+    const int64_t P = kind == APM_KERNEL_ISO ? 2 : d + 1;
+    if (n_theta < P) return fail(nullptr, APM_E_INVALID, "apm_gram: theta too short");
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_tuple(device, n, d, kind + 16);
+    apm_ctx*& c = g_cache[key];
+    try {
+        if (!c) {
+            c = new apm_ctx();
+            init_ctx(c, device, kind, X, n, d, ldx, nullptr, eps, 1, 1, 1, 1);
+        } else {
+            HIPC(hipSetDevice(device));
+            std::vector<double> Xc((size_t)(n * d));
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t k = 0; k < d; ++k) Xc[i * d + k] = X[i * ldx + k];
+            HIPC(hipMemcpyAsync(c->X, Xc.data(), sizeof(double) * n * d, hipMemcpyHostToDevice,
+                                c->stream));
+        }
+        HIPC(hipMemcpyAsync(c->theta, theta, sizeof(double) * P, hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
+        HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+        launch_gram(c->K, c->X, d, (int)n, (int)d, c->theta, P, kind, eps, c->np, live_of(c), 1,
+                    c->stream);
+        check_launch();
+        HIPC(hipMemcpy2DAsync(K, sizeof(double) * ldk, c->K.base, sizeof(double) * c->np,
+                              sizeof(double) * n, n, hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+    } catch (const HipError& e) {
+        if (c) {
+            free_ctx(c);
+            c = nullptr;
+        }
+        return fail(nullptr, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_laplace(int device, const double* K, int64_t n, int64_t ldk, const double* y,
+                int calc_cov, int calc_lml, double diff_f_tol, int64_t max_iters, double* f_out,
+                double* C_out, int64_t ldc, double* lml_out, int64_t* n_iter_out, int* status) {
+    if (!K || !y || n <= 0 || ldk < n || !f_out || !status || max_iters < 0 ||
+        (calc_cov && (!C_out || ldc < n)) || (calc_lml && !lml_out))
+        return fail(nullptr, APM_E_INVALID, "apm_laplace: bad arguments");
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_tuple(device, n, (int64_t)0, (int)APM_KERNEL_PRECOMPUTED);
+    apm_ctx*& c = g_cache[key];
+    try {
+        if (!c) {
+            c = new apm_ctx();
+            init_ctx(c, device, APM_KERNEL_PRECOMPUTED, nullptr, n, 0, 0, y, 1e-8, 1, 1, 1, 1);
+        } else {
+            HIPC(hipSetDevice(device));
+            std::vector<double> yp((size_t)c->np, 0.0);
+            for (int64_t i = 0; i < n; ++i) yp[i] = y[i];
+            HIPC(hipMemcpyAsync(c->y, yp.data(), sizeof(double) * c->np, hipMemcpyHostToDevice,
+                                c->stream));
+        }
+        c->tol = diff_f_tol;
+        c->max_iters = max_iters;
+        const int np = c->np;
+        std::vector<double> Kp((size_t)np * np, 0.0);
+        for (int i = 0; i < np; ++i)
+            for (int j = 0; j < np; ++j)
+                Kp[(size_t)i * np + j] =
+                    (i < n && j < n) ? K[(int64_t)i * ldk + j] : (i == j ? 1.0 : 0.0);
+        HIPC(hipMemcpyAsync(c->K.base, Kp.data(), sizeof(double) * Kp.size(), hipMemcpyHostToDevice,
+                            c->stream));
+        HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
+        HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+        HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int), c->stream));
+        std::vector<int> st(1, 0);
+        newton(c, 1, st);
+        int it = 0;
+        HIPC(hipMemcpyAsync(&it, c->n_iter, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        *status = st[0];
+        if (n_iter_out) *n_iter_out = it;
+        if (st[0] != APM_STATUS_OK) return APM_SUCCESS;
+        HIPC(hipMemcpyAsync(f_out, c->v.f, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+        if (calc_lml) {
+            launch_laplace_lml(c->v, c->y, (int)n, c->ldet, c->lstride, c->nb, c->out, live_of(c),
+                               1, c->stream);
+            check_launch();
+            HIPC(hipMemcpyAsync(lml_out, c->out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        }
+        if (calc_cov) {
+            augmented(c, 1, false);  // bottom-right of A now holds C = K - V^T V (lower)
+            std::vector<double> Cb((size_t)np * np);
+            HIPC(hipMemcpy2DAsync(Cb.data(), sizeof(double) * np,
+                                  c->A.base + (int64_t)np * c->A.ld + np, sizeof(double) * c->A.ld,
+                                  sizeof(double) * np, np, hipMemcpyDeviceToHost, c->stream));
+            sync(c);
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t j = 0; j <= i; ++j) {
+                    C_out[i * ldc + j] = Cb[(size_t)i * np + j];
+                    C_out[j * ldc + i] = Cb[(size_t)i * np + j];
+                }
+        }
+        sync(c);
+    } catch (const HipError& e) {
+        if (c) {
+            free_ctx(c);
+            c = nullptr;
+        }
+        return fail(nullptr, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_selftest_tile(int device, const double* A, const double* B, double* C) {
+    if (!A || !B || !C) return fail(nullptr, APM_E_INVALID, "apm_selftest_tile: null pointer");
+    double* d = nullptr;
+    try {
+        HIPC(hipSetDevice(device));
+        HIPC(hipMalloc(&d, sizeof(double) * 3 * 4096));
+        HIPC(hipMemcpy(d, A, sizeof(double) * 4096, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(d + 4096, B, sizeof(double) * 4096, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(d + 8192, C, sizeof(double) * 4096, hipMemcpyHostToDevice));
+        launch_tile_nt_test(d, d + 4096, d + 8192, nullptr);
+        check_launch();
+        HIPC(hipMemcpy(C, d + 8192, sizeof(double) * 4096, hipMemcpyDeviceToHost));
+        HIPC(hipFree(d));
+    } catch (const HipError& e) {
+        if (d) (void)hipFree(d);
+        return fail(nullptr, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+int apm_prof_enable(apm_ctx* c, int on) {
+    if (!c) return fail(c, APM_E_INVALID, "apm_prof_enable: null ctx");
+    c->prof = on != 0;
+    return APM_SUCCESS;
+}
+
+int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, double* work,
+                  int reset) {
+    if (!c || kind < 0 || kind >= APM_PROF_NKINDS)
+        return fail(c, APM_E_INVALID, "apm_prof_read: bad arguments");
+    try {
+        HIPC(hipSetDevice(c->device));
+        sync(c);
+        double ms = 0.0, wk = 0.0;
+        int64_t cnt = 0;
+        for (const ProfRec& r : c->recs) {
+            if (r.kind != kind) continue;
+            float e = 0.f;
+            HIPC(hipEventElapsedTime(&e, r.a, r.b));
+            ms += e;
+            wk += r.work;
+            ++cnt;
+        }
+        if (total_ms) *total_ms = ms;
+        if (launches) *launches = cnt;
+        if (work) *work = wk;
+        if (reset) {
+            c->recs.clear();
+            c->evnext = 0;
+        }
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,321 @@
+// Laplace-approximation Newton iteration (fp64) and the theta-call plumbing around the Cholesky.
+//
+// Follows gpdemo/latent_posterior_approximations.py:81-124 (Rasmussen & Williams Alg. 3.1 form):
+//   v = phi(f)/Phi(yf) (:86), grad = v y, W = v^2 + grad f (:87-88), B = I + W^1/2 K W^1/2 (:89-91),
+//   L = chol(B) (:92), b = W f + grad (:93), a = b - W^1/2 L^-T L^-1 W^1/2 K b (:94), f <- K a (:95),
+//   stop when mean((f_new - f)^2) < tol (:96-97).
+// The forward solve L^-1 (W^1/2 K b) is produced by the Cholesky itself: W^1/2 K b is appended as an
+// extra row below B, so the factorisation of the (np+64) x np trapezoid returns it in that row.
+#include "apm_internal.h"
+
+__device__ __forceinline__ bool live_b(const Live& lv, int b) {
+    return lv.active[b] != 0 && lv.status[b] == 0;
+}
+
+// ------------------------------------------------------------------------------- vectors
+__global__ __launch_bounds__(256) void k_newton_prep(NewtonVecs v, const double* __restrict__ y,
+                                                     int n, int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= np) return;
+    const int64_t o = b * v.vstride + i;
+    double W = 0.0, Ws = 0.0, bb = 0.0;
+    if (i < n) {
+        const double f = v.f[o], yi = y[i];
+        const double vv = exp(-0.5 * f * f - log_ndtr_d(yi * f) - 0.91893853320467274178);
+        const double grad = vv * yi;
+        W = vv * vv + grad * f;
+        Ws = sqrt(W);
+        bb = W * f + grad;
+    }
+    v.W[o] = W;
+    v.Ws[o] = Ws;
+    v.b[o] = bb;
+}
+
+void launch_newton_prep(NewtonVecs v, const double* y, int n, int np, Live live, int nchains,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_newton_prep, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, y, n,
+                       np, live);
+}
+
+// out = M x for a full np x np row-major M; one wave per row, 16-byte loads
+__global__ __launch_bounds__(256) void k_gemv(MatB M, const double* __restrict__ x,
+                                              int64_t xstride, double* __restrict__ out,
+                                              int64_t ostride, int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const double* xb = x + b * xstride;
+    for (int row = blockIdx.x * 16 + w * 4; row < blockIdx.x * 16 + w * 4 + 4; ++row) {
+        const double* Mr = M.base + b * M.cstride + (int64_t)row * M.ld;
+        double s = 0.0;
+        for (int c = lane * 2; c < np; c += 128) {
+            const d2_t m = *reinterpret_cast<const d2_t*>(Mr + c);
+            const d2_t xx = *reinterpret_cast<const d2_t*>(xb + c);
+            s = fma(m.x, xx.x, s);
+            s = fma(m.y, xx.y, s);
+        }
+        s = wave_sum_d(s);
+        if (lane == 0) out[b * ostride + row] = s;
+    }
+}
+
+void launch_gemv(MatB M, const double* x, int64_t xstride, double* out, int64_t ostride, int np,
+                 Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_gemv, dim3(np / 16, nchains), dim3(256), 0, s, M, x, xstride, out,
+                       ostride, np, live);
+}
+
+__device__ __forceinline__ void tri_decode(int t, int& ti, int& tj) {
+    int i = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (i * (i + 1) / 2 > t) --i;
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    ti = i;
+    tj = t - i * (i + 1) / 2;
+}
+
+// B = I + W^1/2 K W^1/2 into the lower tiles of A's top-left np x np, and the extra row block
+// rows [np, np+64): row np = W^1/2 (K b) (the Newton right-hand side), the others zero.
+__global__ __launch_bounds__(256) void k_form_B(MatB K, MatB A, NewtonVecs v, int nb,
+                                                Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    const int t = blockIdx.x, ntri = nb * (nb + 1) / 2;
+    const double* Kb = K.base + b * K.cstride;
+    double* Ab = A.base + b * A.cstride;
+    const double* Ws = v.Ws + b * v.vstride;
+    const int tid = threadIdx.x;
+    if (t < ntri) {
+        int ti, tj;
+        tri_decode(t, ti, tj);
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
+            const double kv = Kb[(int64_t)r * K.ld + c];
+            Ab[(int64_t)r * A.ld + c] = (r == c ? 1.0 : 0.0) + (Ws[r] * kv) * Ws[c];
+        }
+    } else {
+        const int tj = t - ntri;
+        const int64_t r0 = (int64_t)nb * 64;
+        const double* Kbv = v.Kb + b * v.vstride;
+        for (int e = tid; e < 4096; e += 256) {
+            const int rr = e >> 6, c = tj * 64 + (e & 63);
+            Ab[(r0 + rr) * A.ld + c] = (rr == 0) ? Ws[c] * Kbv[c] : 0.0;
+        }
+    }
+}
+
+void launch_form_B(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_form_B, dim3(nb * (nb + 1) / 2 + nb, nchains), dim3(256), 0, s, K, A, v,
+                       nb, live);
+}
+
+__global__ __launch_bounds__(256) void k_newton_update(NewtonVecs v, int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= np) return;
+    const int64_t o = b * v.vstride + i;
+    v.a[o] = v.b[o] - v.Ws[o] * v.z[o];
+}
+
+void launch_newton_update(NewtonVecs v, int np, Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_newton_update, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, np,
+                       live);
+}
+
+// diff = mean((f_new - f)^2) over the n real entries; f <- f_new; converged chains drop out.
+__global__ __launch_bounds__(256) void k_newton_check(NewtonVecs v, int n, int np, double tol,
+                                                      int* active, const int* status,
+                                                      int* n_iter) {
+    const int b = blockIdx.x;
+    if (active[b] == 0 || status[b] != 0) return;
+    __shared__ double red[4];
+    const double* fn = v.fnew + b * v.vstride;
+    double* f = v.f + b * v.vstride;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double d = fn[i] - f[i];
+        s += d * d;
+    }
+    s = block_sum_d(s, red);
+    __syncthreads();
+    for (int i = threadIdx.x; i < np; i += 256) f[i] = fn[i];
+    if (threadIdx.x == 0) {
+        n_iter[b] += 1;
+        if (s / n < tol) active[b] = 0;
+    }
+}
+
+void launch_newton_check(NewtonVecs v, int n, int np, double tol, int* active, const int* status,
+                         int* n_iter, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_newton_check, dim3(nchains), dim3(256), 0, s, v, n, np, tol, active,
+                       status, n_iter);
+}
+
+// lower tiles of src's np x np -> dst (PriorMC: factor K itself)
+__global__ __launch_bounds__(256) void k_copy_lower(MatB src, MatB dst, Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    int ti, tj;
+    tri_decode(blockIdx.x, ti, tj);
+    const double* S = src.base + b * src.cstride;
+    double* D = dst.base + b * dst.cstride;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
+        D[(int64_t)r * dst.ld + c] = S[(int64_t)r * src.ld + c];
+    }
+}
+
+void launch_copy_lower(MatB src, MatB dst, int np, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_copy_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, src, dst,
+                       live);
+}
+
+// Augmented matrix for the posterior covariance factor:
+//   [[ B          .  ]        chol       [[ L      0      ]
+//    [ K W^1/2    K  ]   ---------->      [ V^T    C_chol ]      V = L^-1 W^1/2 K,
+//    [ 0      f_post^T]]                  [ 0      g^T    ]]     C = K - V^T V, g = C_chol^-1 f_post
+// The top-left (L of the last Newton iteration) is already factored; this fills rows [np, 2np+64).
+__global__ __launch_bounds__(256) void k_form_aug(MatB K, MatB A, NewtonVecs v, int nb,
+                                                  Live live) {
+    const int b = blockIdx.y;
+    if (!live_b(live, b)) return;
+    const int t = blockIdx.x;
+    const int nbl = nb * nb, ntri = nb * (nb + 1) / 2;
+    const double* Kb = K.base + b * K.cstride;
+    double* Ab = A.base + b * A.cstride;
+    const double* Ws = v.Ws + b * v.vstride;
+    const int64_t np = (int64_t)nb * 64;
+    const int tid = threadIdx.x;
+    if (t < nbl) {  // bottom-left: (K W^1/2)[r][c] = K[r][c] * W^1/2[c]
+        const int ti = t / nb, tj = t % nb;
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
+            Ab[(np + r) * A.ld + c] = Kb[(int64_t)r * K.ld + c] * Ws[c];
+        }
+    } else if (t < nbl + ntri) {  // bottom-right lower tiles: K
+        int ti, tj;
+        tri_decode(t - nbl, ti, tj);
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
+            Ab[(np + r) * A.ld + np + c] = Kb[(int64_t)r * K.ld + c];
+        }
+    } else {  // extra row block at 2np: row 0 = [0 | f_post^T]
+        const int tj = t - nbl - ntri;  // 0 .. 2nb-1
+        const double* f = v.f + b * v.vstride;
+        for (int e = tid; e < 4096; e += 256) {
+            const int rr = e >> 6, c = tj * 64 + (e & 63);
+            Ab[(2 * np + rr) * A.ld + c] = (rr == 0 && c >= np) ? f[c - np] : 0.0;
+        }
+    }
+}
+
+void launch_form_aug(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains,
+                     hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_form_aug, dim3(nb * nb + nb * (nb + 1) / 2 + 2 * nb, nchains), dim3(256),
+                       0, s, K, A, v, nb, live);
+}
+
+// Laplace LML (latent_posterior_approximations.py:103-106), with -sum log L_ii = -sum_k ldet[k]
+__global__ __launch_bounds__(256) void k_laplace_lml(NewtonVecs v, const double* __restrict__ y,
+                                                     int n, const double* ldet, int64_t lstride,
+                                                     int nb, double* out, Live live) {
+    const int b = blockIdx.x;
+    if (live.status[b] != 0) return;
+    __shared__ double red[4];
+    const double* f = v.f + b * v.vstride;
+    const double* a = v.a + b * v.vstride;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        s1 += a[i] * f[i];
+        s2 += log_ndtr_d(y[i] * f[i]);
+    }
+    s1 = block_sum_d(s1, red);
+    __syncthreads();
+    s2 = block_sum_d(s2, red);
+    if (threadIdx.x == 0) {
+        double ld = 0.0;
+        for (int k = 0; k < nb; ++k) ld += ldet[b * lstride + k];
+        out[b] = -0.5 * s1 + s2 - ld;
+    }
+}
+
+void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet,
+                        int64_t lstride, int nb, double* out, Live live, int nchains,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_laplace_lml, dim3(nchains), dim3(256), 0, s, v, y, n, ldet, lstride, nb,
+                       out, live);
+}
+
+// ------------------------------------------------------------------------------- cache slots
+// mode 0 (IS):      L = C_chol (A rows/cols offset np), row np of L = g^T (A row 2np, cols >= np)
+// mode 1 (PriorMC): L = K_chol (A top-left), row np of L = 0
+// Rows are written whole (upper part zero) because the u-path GEMM streams full row segments.
+__global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
+                                                      const int64_t* __restrict__ slots, int mode,
+                                                      int np, Live live) {
+    const int b = blockIdx.y;
+    if (live.status[b] != 0) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 4 + w;  // 0 .. np+63
+    const double* Ab = A.base + b * A.cstride;
+    float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
+    const int64_t off = (mode == 0) ? np : 0;
+    if (r < np) {
+        const double* src = Ab + (off + r) * A.ld + off;
+        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? (float)src[c] : 0.0f;
+    } else if (r == np && mode == 0) {
+        const double* src = Ab + (2 * (int64_t)np) * A.ld + np;
+        for (int c = lane; c < np; c += 64) L[c] = (float)src[c];
+    } else {
+        for (int c = lane; c < np; c += 64) L[c] = 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, const double* ldet,
+                                                        int64_t lstride, int nb, SlotSet S,
+                                                        const int64_t* __restrict__ slots,
+                                                        int mode, int n, Live live) {
+    const int b = blockIdx.x;
+    if (live.status[b] != 0) return;
+    __shared__ double red[4];
+    const int64_t np = (int64_t)nb * 64;
+    const int64_t so = slots[b] * S.vstride;
+    double gg = 0.0;
+    for (int i = threadIdx.x; i < np; i += 256) {
+        const bool is = (mode == 0) && i < n;
+        const double f = is ? v.f[b * v.vstride + i] : 0.0;
+        const double W = is ? v.W[b * v.vstride + i] : 0.0;
+        S.fpost[so + i] = (float)f;
+        S.fpost64[so + i] = f;
+        S.W[so + i] = (float)W;
+        if (mode == 0) {
+            const double g = A.base[b * A.cstride + 2 * np * A.ld + np + i];
+            gg += g * g;
+        }
+    }
+    gg = block_sum_d(gg, red);
+    if (threadIdx.x == 0) {
+        double c = 0.0;
+        if (mode == 0) {
+            double ld = 0.0;
+            for (int k = 0; k < nb; ++k) ld += ldet[b * lstride + k];
+            c = -0.5 * gg - ld;
+        }
+        S.cst[slots[b]] = c;
+    }
+}
+
+void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
+                       SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
+                       int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_slot_write_L, dim3((np + 64) / 4, nchains), dim3(256), 0, s, A, S, slots,
+                       mode, np, live);
+    hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
+                       S, slots, mode, n, live);
+}

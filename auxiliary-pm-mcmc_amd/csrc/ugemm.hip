@@ -1,0 +1,266 @@
+// Importance-sampling u-path: f_s = f_post + L U (fp32 MFMA), probit epilogue, log-mean-exp.
+//
+// Replaces gpdemo/estimators.py:221-241 (ApproxPosteriorIS, theta- and cached u-calls) and
+// :323-325 (PriorMC) in the algebraically identical form of DESIGN.md §3:
+//   log w_s = sum_n [log Phi(y_n f_sn) + 1/2 W_n f_sn^2] - g^T u_s + cst,
+//   cst = -1/2 |g|^2 - 1/2 log|B|          (IS);     W = 0, g = 0, cst = 0   (PriorMC)
+// g^T u_s comes out of the same GEMM: g^T is stored as row np of the slot's factor, so the extra
+// 64-row block of the output holds it in its first row.
+#include "apm_internal.h"
+
+// ------------------------------------------------------------------------------- U buffers
+__global__ __launch_bounds__(256) void k_u_convert(const double* __restrict__ U, int64_t ldu,
+                                                   int n, int S, float* __restrict__ dst, int sp,
+                                                   int np) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)np * sp) return;
+    const int r = (int)(e / sp), c = (int)(e % sp);
+    dst[e] = (r < n && c < S) ? (float)U[(int64_t)r * ldu + c] : 0.0f;
+}
+
+void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int64_t ubuf,
+                      hipStream_t s) {
+    const int np = (int)(P.stride / P.sp);
+    const int64_t tot = (int64_t)np * P.sp;
+    hipLaunchKernelGGL(k_u_convert, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, U64, ldu,
+                       n, S, P.base + ubuf * P.stride, P.sp, np);
+}
+
+// Philox4x32-10 (Salmon et al., SC'11) + Box-Muller: counter = (e/4, ctr_lo, ctr_hi, 0)
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_u_normal(UPool P, const int64_t* __restrict__ ubufs,
+                                                  const uint64_t* __restrict__ seeds,
+                                                  const uint64_t* __restrict__ counters, int n,
+                                                  int S) {
+    const int b = blockIdx.y;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // group of 4 normals
+    const int64_t tot = (int64_t)n * S;
+    if (q * 4 >= tot) return;
+    const uint64_t sd = seeds[b], ct = counters[b];
+    uint32_t c[4] = {(uint32_t)q, (uint32_t)ct, (uint32_t)(ct >> 32), (uint32_t)(q >> 32)};
+    philox4x32_10(c, (uint32_t)sd, (uint32_t)(sd >> 32));
+    float z[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const float u1 = ((float)c[2 * h] + 0.5f) * 2.3283064365386963e-10f;
+        const float u2 = ((float)c[2 * h + 1] + 0.5f) * 2.3283064365386963e-10f;
+        const float rr = sqrtf(-2.0f * logf(u1));
+        float sn, cs;
+        sincosf(6.283185307179586f * u2, &sn, &cs);
+        z[2 * h] = rr * cs;
+        z[2 * h + 1] = rr * sn;
+    }
+    float* dst = P.base + ubufs[b] * P.stride;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int64_t e = q * 4 + h;
+        if (e < tot) dst[(e / S) * P.sp + (e % S)] = z[h];
+    }
+}
+
+void launch_u_normal(UPool P, const int64_t* ubufs, const uint64_t* seeds,
+                     const uint64_t* counters, int n, int S, int nchains, hipStream_t s) {
+    const int64_t groups = ((int64_t)n * S + 3) / 4;
+    hipLaunchKernelGGL(k_u_normal, dim3((unsigned)((groups + 255) / 256), nchains), dim3(256), 0, s,
+                       P, ubufs, seeds, counters, n, S);
+}
+
+__global__ __launch_bounds__(256) void k_u_combine(UPool P, const int64_t* __restrict__ dst,
+                                                   const int64_t* __restrict__ a,
+                                                   const int64_t* __restrict__ bb,
+                                                   const double* __restrict__ ca,
+                                                   const double* __restrict__ cb, int64_t tot) {
+    const int b = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= tot) return;
+    const float x = P.base[a[b] * P.stride + e], v = P.base[bb[b] * P.stride + e];
+    P.base[dst[b] * P.stride + e] = (float)ca[b] * x + (float)cb[b] * v;
+}
+
+void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64_t* b,
+                      const double* ca, const double* cb, int n, int S, int nchains,
+                      hipStream_t s) {
+    (void)n;
+    (void)S;
+    const int64_t tot = P.stride;  // padded entries are 0 in both inputs, stay 0
+    hipLaunchKernelGGL(k_u_combine, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0, s,
+                       P, dst, a, b, ca, cb, tot);
+}
+
+// ------------------------------------------------------------------------------- L . U + epilogue
+// v_mfma_f32_16x16x4_f32: A lane l -> A[l&15][k=l>>4], B lane l -> B[k=l>>4][l&15],
+// C/D lane l, reg r -> (row = (l>>4)*4 + r, col = l&15)
+#define UP 65  // LDS row pitch (floats) of the staged U tile: conflict-free B-fragment reads
+
+__global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restrict__ slots,
+                                               UPool P, const int64_t* __restrict__ ubufs,
+                                               const double* __restrict__ y, int n, int np,
+                                               double* __restrict__ partial, int64_t pstride,
+                                               const int* __restrict__ status) {
+    const int b = blockIdx.z;
+    if (status[b] != 0) return;
+    const int nb = np / 64;
+    const int i = nb - (int)blockIdx.x;  // heaviest row blocks (longest K range) first
+    const int sb = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    __shared__ float Ut[64][UP];
+    __shared__ double csum[2][64];
+
+    const int64_t slot = slots[b];
+    const float* L = S.L + slot * S.lstride;
+    const float* U = P.base + ubufs[b] * P.stride;
+    const int sp = P.sp;
+    const int kend = (i == nb) ? np : (i + 1) * 64;
+
+    f4_t acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int kk = 0; kk < kend; kk += 64) {
+        __syncthreads();
+        // stage U[kk:kk+64][sb*64 : sb*64+64] (16 KB) with 16-byte loads
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int e = tid + h * 256;  // float4 index 0..1023
+            const int r = e >> 4, c4 = (e & 15) * 4;
+            const f4_t v = *reinterpret_cast<const f4_t*>(U + (int64_t)(kk + r) * sp + sb * 64 + c4);
+            Ut[r][c4] = v[0];
+            Ut[r][c4 + 1] = v[1];
+            Ut[r][c4 + 2] = v[2];
+            Ut[r][c4 + 3] = v[3];
+        }
+        // A fragments straight from global: 16 contiguous floats per lane and row
+        float a[2][16];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+            const float* p = L + (int64_t)(i * 64 + 32 * wr + 16 * bi + r16) * np + kk + kq * 16;
+#pragma unroll
+            for (int t = 0; t < 16; t += 4) {
+                const f4_t v = *reinterpret_cast<const f4_t*>(p + t);
+                a[bi][t] = v[0];
+                a[bi][t + 1] = v[1];
+                a[bi][t + 2] = v[2];
+                a[bi][t + 3] = v[3];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            float bv[2];
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) bv[bj] = Ut[kq * 16 + t][32 * wc + 16 * bj + r16];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi][t], bv[bj],
+                                                                       acc[bi][bj], 0, 0, 0);
+        }
+    }
+
+    double* pb = partial + b * pstride;
+    if (i == nb) {
+        // g^T u_s sits in output row np = first row of this block: wr=0, bi=0, lane>>4=0, r=0
+        if (wr == 0 && kq == 0) {
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+                pb[(int64_t)nb * sp + sb * 64 + 32 * wc + 16 * bj + r16] = (double)acc[0][bj][0];
+        }
+        return;
+    }
+    const float* fp = S.fpost + slot * S.vstride;
+    const float* Wv = S.W + slot * S.vstride;
+    double colsum[2];
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+        float s = 0.f;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = i * 64 + 32 * wr + 16 * bi + kq * 4 + r;
+                if (row < n) {
+                    const float f = fp[row] + acc[bi][bj][r];
+                    s += log_ndtr_f((float)y[row] * f) + 0.5f * Wv[row] * f * f;
+                }
+            }
+        double d = (double)s;
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        colsum[bj] = d;
+    }
+    if (kq == 0) {
+        csum[wr][32 * wc + r16] = colsum[0];
+        csum[wr][32 * wc + 16 + r16] = colsum[1];
+    }
+    __syncthreads();
+    if (tid < 64) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
+}
+
+void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
+                  const double* y, int n, int np, double* partial, int64_t pstride,
+                  const int* status, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_ugemm, dim3(nb + 1, P.sp / 64, nchains), dim3(256), 0, s, S, slots, P,
+                       ubufs, y, n, np, partial, pstride, status);
+}
+
+// logsumexp_s(lw_s) - log S per chain
+__global__ __launch_bounds__(256) void k_lme(const double* __restrict__ partial, int64_t pstride,
+                                             int nb, int S, int sp, SlotSet Sl,
+                                             const int64_t* __restrict__ slots,
+                                             double* __restrict__ out,
+                                             const int* __restrict__ status) {
+    const int b = blockIdx.x;
+    if (status[b] != 0) return;
+    __shared__ double red[4];
+    __shared__ double lw[1024];
+    const double* pb = partial + b * pstride;
+    const double cst = Sl.cst[slots[b]];
+    double mx = -INFINITY;
+    for (int s = threadIdx.x; s < S; s += 256) {
+        double v = cst - pb[(int64_t)nb * sp + s];
+        for (int i = 0; i < nb; ++i) v += pb[(int64_t)i * sp + s];
+        if (s < 1024) lw[s] = v;
+        mx = fmax(mx, v);
+    }
+    mx = block_max_d(mx, red);
+    __syncthreads();
+    double se = 0.0;
+    for (int s = threadIdx.x; s < S; s += 256) {
+        double v;
+        if (s < 1024) {
+            v = lw[s];
+        } else {
+            v = cst - pb[(int64_t)nb * sp + s];
+            for (int i = 0; i < nb; ++i) v += pb[(int64_t)i * sp + s];
+        }
+        se += exp(v - mx);
+    }
+    se = block_sum_d(se, red);
+    if (threadIdx.x == 0) out[b] = (isfinite(mx) ? mx + log(se) : mx) - log((double)S);
+}
+
+void launch_lme(const double* partial, int64_t pstride, int nb, int S, int sp, SlotSet Sl,
+                const int64_t* slots, double* out, const int* status, int nchains,
+                hipStream_t s) {
+    hipLaunchKernelGGL(k_lme, dim3(nchains), dim3(256), 0, s, partial, pstride, nb, S, sp, Sl,
+                       slots, out, status);
+}

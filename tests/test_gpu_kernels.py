@@ -1,0 +1,151 @@
+"""GPU parity of the HIP building blocks through the C-ABI (libapm.so) against the oracle and
+the golden vectors produced by the reference (tests/golden/make_golden.py).
+
+Tolerances: theta-path quantities are fp64 (Gram 1e-13 rel; Laplace f 1e-9 rel);
+estimator values go through the fp32 MFMA L.U and are checked to |d log f| <= 2e-3 + 2e-5 |log f|.
+"""
+import numpy as np
+import pytest
+
+import apm_oracle as orc
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_ABS, TOL_REL = 2e-3, 2e-5
+
+
+def _close(v, ref):
+    return abs(v - ref) <= TOL_ABS + TOL_REL * abs(ref)
+
+
+@pytest.fixture(scope='module')
+def nat(gpu_available):
+    from gpdemo import _native
+    _native.load_library()
+    return _native
+
+
+def _cases():
+    g = golden('estimators')
+    out = []
+    for ci in range(int(g['n_cases'])):
+        pre = 'c{0}_'.format(ci)
+        out.append({k[len(pre):]: g[k] for k in g.files if k.startswith(pre)})
+    return out
+
+
+def test_mfma_f64_tile_layout(nat):
+    rng = np.random.RandomState(0)
+    A = rng.normal(size=(64, 64))
+    B = rng.normal(size=(64, 64)) + np.arange(64)[:, None] * 0.01  # asymmetric
+    C = rng.normal(size=(64, 64))
+    out = nat.selftest_tile(A, B, C)
+    np.testing.assert_allclose(out, C + A.dot(B.T), rtol=1e-12, atol=1e-12)
+
+
+def test_gram_vs_golden(nat):
+    g = golden('gram')
+    keys = sorted({k.rsplit('_', 1)[0] for k in g.files if k.endswith('_thetas')})
+    for key in keys:
+        kind = nat.KERNEL_ISO if key.startswith('iso') else nat.KERNEL_ARD
+        X = g[key + '_X']
+        for th, Kref in zip(g[key + '_thetas'], g[key + '_K']):
+            K = np.empty_like(Kref)
+            nat.gram(kind, K, X, th, 1e-8)
+            np.testing.assert_allclose(K, Kref, rtol=1e-13, atol=1e-300)
+
+
+def test_gram_large_ragged_vs_c_oracle(nat):
+    rng = np.random.RandomState(5)
+    for n, d in ((300, 7), (1000, 32), (129, 64)):
+        X = rng.normal(size=(n, d))
+        th = np.r_[0.3, rng.normal(size=d)]
+        K = np.empty((n, n))
+        nat.gram(nat.KERNEL_ARD, K, X, th, 1e-8)
+        Kr = np.empty((n, n))
+        orc.c_gram('ard', Kr, X, th, 1e-8)
+        np.testing.assert_allclose(K, Kr, rtol=1e-13, atol=1e-300)
+
+
+def test_laplace_vs_golden(nat):
+    for c in _cases():
+        f, C, lml, nit, st = nat.laplace(c['K'], c['y'], True, True, 1e-4, 1000)
+        assert st == 0
+        assert nit + 1 == int(c['lap_nops_cov_lml'])
+        np.testing.assert_allclose(f, c['lap_f'], rtol=1e-9, atol=1e-11)
+        np.testing.assert_allclose(C, c['lap_C'], rtol=1e-8, atol=1e-10)
+        assert abs(lml - float(c['lap_lml'])) < 1e-8 * max(1., abs(float(c['lap_lml'])))
+
+
+def _ctx(nat, c, n_slots=4, n_ubufs=4, max_batch=1):
+    kind = nat.KERNEL_ISO if str(c['kind']) == 'iso' else nat.KERNEL_ARD
+    return nat.Context(c['X'], c['y'], kind, 1e-8, c['ns1'].shape[1], max_batch=max_batch,
+                       n_slots=n_slots, n_ubufs=n_ubufs)
+
+
+def test_is_estimator_vs_golden(nat):
+    for ci, c in enumerate(_cases()):
+        ctx = _ctx(nat, c)
+        ctx.u_upload(0, c['ns1'])
+        ctx.u_upload(1, c['ns2'])
+        out, st, nops = ctx.theta_eval(nat.EST_IS, c['theta'][None], [0], [0])
+        assert st[0] == 0
+        assert nops[0] == int(c['is_ops'])
+        assert _close(out[0], float(c['is_logf1'])), (ci, out[0], float(c['is_logf1']))
+        out2, st2 = ctx.u_eval([0], [1])
+        assert _close(out2[0], float(c['is_logf2'])), (ci, out2[0], float(c['is_logf2']))
+        L, f, g, cst = ctx.slot_read(0)
+        np.testing.assert_allclose(f, c['f_post'], rtol=1e-8, atol=1e-10)
+        np.testing.assert_allclose(L, np.tril(c['C_chol']), rtol=0, atol=2e-6 * np.abs(c['C_chol']).max())
+        ctx.close()
+
+
+def test_priormc_and_laplace_estimators_vs_golden(nat):
+    for ci, c in enumerate(_cases()):
+        ctx = _ctx(nat, c)
+        ctx.u_upload(0, c['ns1'])
+        ctx.u_upload(1, c['ns2'])
+        out, st, nops = ctx.theta_eval(nat.EST_PRIORMC, c['theta'][None], [0], [0])
+        assert st[0] == 0 and nops[0] == 1
+        assert _close(out[0], float(c['pmc_logf1'])), (ci, out[0], float(c['pmc_logf1']))
+        out2, _ = ctx.u_eval([0], [1])
+        assert _close(out2[0], float(c['pmc_logf2'])), (ci, out2[0], float(c['pmc_logf2']))
+        lml, st, nops = ctx.theta_eval(nat.EST_LAPLACE, c['theta'][None])
+        assert st[0] == 0 and nops[0] == int(c['lapest_ops'])
+        assert abs(lml[0] - float(c['lapest_lml'])) < 1e-8 * max(1, abs(lml[0]))
+        ctx.close()
+
+
+def test_batched_equals_single(nat):
+    c = _cases()[1]
+    ctx = _ctx(nat, c, n_slots=6, n_ubufs=6, max_batch=3)
+    ctx.u_upload(0, c['ns1'])
+    ctx.u_upload(1, c['ns2'])
+    th = np.stack([c['theta'], c['theta'] + 0.1, c['theta'] - 0.2])
+    out, st, nops = ctx.theta_eval(nat.EST_IS, th, [0, 1, 0], [0, 1, 2])
+    assert (st == 0).all()
+    for b in range(3):
+        o1, s1, _ = ctx.theta_eval(nat.EST_IS, th[b][None], [[0, 1, 0][b]], [3])
+        assert abs(o1[0] - out[b]) < 1e-9 * max(1., abs(out[b]))
+    # reference values at the perturbed thetas
+    kf = orc.make_kernel_func('ard', 1e-8)
+    for b in range(3):
+        ns = c['ns1'] if b != 1 else c['ns2']
+        v, _, _ = orc.is_estimate(c['X'], c['y'], kf, ns, th[b])
+        assert _close(out[b], v), (b, out[b], v)
+    ctx.close()
+
+
+def test_u_normal_moments(nat):
+    c = _cases()[2]
+    ctx = _ctx(nat, c)
+    ctx.u_normal([0, 1], [123, 123], [0, 1])
+    U0, U1 = ctx.u_download(0), ctx.u_download(1)
+    assert abs(U0.mean()) < 0.02 and abs(U0.std() - 1) < 0.02
+    assert not np.allclose(U0, U1)
+    ctx.u_normal([2], [123], [0])
+    np.testing.assert_array_equal(ctx.u_download(2), U0)  # counter-based: reproducible
+    ctx.u_combine([3], [0], [1], [0.6], [0.8])
+    np.testing.assert_allclose(ctx.u_download(3), 0.6 * U0 + 0.8 * U1, rtol=1e-5, atol=1e-5)
+    ctx.close()
