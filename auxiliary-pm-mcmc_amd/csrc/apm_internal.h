@@ -21,13 +21,15 @@ struct Live {
 // diag:   factor tile (k,k) in place, write its inverse to Dinv[b][k] and sum(log diag) to
 //         ldet[b][k]; a non-positive pivot sets status[b] = fail_code.
 // panel:  tiles (i,k), i in [i0, R):  A_ik <- A_ik * inv(L_kk)^T     (f64 MFMA)
-// update: tiles (i,j), i in [i0, R), k < j <= min(i, Cb-1):  A_ij -= A_ik A_jk^T  (f64 MFMA)
+// update: tiles (i,j), i in [i0, R), j0 <= j <= min(i, jend-1):
+//         A_ij -= sum_{q<kc} A_{i,k0+q} A_{j,k0+q}^T  (f64 MFMA, rank 64*kc)
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
                       Live live, int fail_code, int nchains, hipStream_t s);
 void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
                        Live live, int nchains, hipStream_t s);
-void launch_chol_update(MatB A, int k, int i0, int R, int Cb, Live live, int nchains,
-                        hipStream_t s);
+void launch_chol_update(MatB A, int k0, int kc, int i0, int R, int j0, int jend, Live live,
+                        int nchains, hipStream_t s);
+long update_tile_count(int i0, int R, int j0, int jend);
 // one step (block J) of the backward solve L^T z = r, r stored in row `rrow` of A (in place),
 // z written to z[b*zstride + ...]
 void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,

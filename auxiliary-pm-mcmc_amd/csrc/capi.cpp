@@ -126,32 +126,50 @@ struct ProfScope {
 // ------------------------------------------------------------------------------- building blocks
 Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
 
+// Two-level right-looking Cholesky over tile columns [k0, k1) of rows < R (tile units), the
+// trailing matrix spanning columns < Cb. Outer panels of OUTER tiles (256 columns) are factored
+// with the 64-wide diag / panel / inner-update steps; the rest of the matrix then receives one
+// rank-256 update per outer panel (4x less read-modify-write traffic than rank-64 steps).
+// row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
+// augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
+static const int OUTER = 4;
+
+double update_flops(int i0, int R, int j0, int jend, int kc) {
+    double f = 0.0;
+    for (int i = i0; i < R; ++i) {
+        const int jmax = std::min(i, jend - 1);
+        for (int j = j0; j <= jmax; ++j)
+            f += (i == j) ? 64.0 * 65.0 * 64.0 * kc : 2.0 * 64.0 * 64.0 * 64.0 * kc;
+    }
+    return f;
+}
+
+void tracked_update(apm_ctx* c, int k0, int kc, int i0, int R, int j0, int jend, int count) {
+    if (i0 < j0) i0 = j0;
+    if (update_tile_count(i0, R, j0, jend) <= 0) return;
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE,
+                 c->prof ? update_flops(i0, R, j0, jend, kc) * count : 0.0);
+    launch_chol_update(c->A, k0, kc, i0, R, j0, jend, live_of(c), count, c->stream);
+    check_launch();
+}
+
 void chol_range(apm_ctx* c, int k0, int k1, int R, int Cb, int fail_code, int count,
                 bool factor_diag = true, int row_start = 0) {
     const Live lv = live_of(c);
-    for (int k = k0; k < k1; ++k) {
-        const int i0 = std::max(k + 1, row_start);
-        if (factor_diag) {
-            launch_chol_diag(c->A, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
-                             count, c->stream);
-            check_launch();
-        }
-        launch_chol_panel(c->A, k, i0, R, c->Dinv, c->dstride, lv, count, c->stream);
-        check_launch();
-        // algorithmic flops of this trailing update: off-diagonal tiles 2*64^3, diagonal tiles
-        // 64*65*64 (lower half), summed over the tiles actually updated
-        double flops = 0.0;
-        if (c->prof) {
-            for (int i = i0; i < R; ++i) {
-                const int jmax = std::min(i, Cb - 1);
-                for (int j = k + 1; j <= jmax; ++j)
-                    flops += (i == j) ? 64.0 * 65.0 * 64.0 : 2.0 * 64.0 * 64.0 * 64.0;
+    for (int K = k0; K < k1; K += OUTER) {
+        const int Kend = std::min(K + OUTER, k1);
+        for (int k = K; k < Kend; ++k) {
+            if (factor_diag) {
+                launch_chol_diag(c->A, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv,
+                                 fail_code, count, c->stream);
+                check_launch();
             }
-            flops *= count;
+            launch_chol_panel(c->A, k, std::max(k + 1, row_start), R, c->Dinv, c->dstride, lv,
+                              count, c->stream);
+            check_launch();
+            tracked_update(c, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, count);
         }
-        ProfScope ps(c, APM_PROF_CHOL_UPDATE, flops);
-        launch_chol_update(c->A, k, i0, R, Cb, lv, count, c->stream);
-        check_launch();
+        tracked_update(c, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb, count);
     }
 }
 

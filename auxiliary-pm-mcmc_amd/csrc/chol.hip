@@ -5,6 +5,8 @@
 //   la.cholesky(C)  gpdemo/estimators.py:209        la.cho_solve(L, .)  latent_posterior_approximations.py:94
 // The work matrix is tiled TB x TB (TB = 64). One workgroup (4 waves) owns one output tile; each
 // wave owns a 32x32 quadrant = 2x2 v_mfma_f64_16x16x4_f64 accumulators.
+#include <algorithm>
+
 #include "apm_internal.h"
 
 // v_mfma_f64_16x16x4_f64 operand/result maps (cdna_hip_programming.md §3):
@@ -82,59 +84,150 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 }
 
 // ------------------------------------------------------------------------------- diagonal tile
-// Unblocked right-looking Cholesky of the 64x64 tile in LDS (256 threads), then the inverse of
-// the lower factor by one wave with the column held in registers (fully unrolled substitution).
+// Broadcast lane l's value of a wave-uniform-indexed register (v_readlane x2).
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// 64x64 Cholesky + inverse of the lower factor in one workgroup (LDS resident), blocked by 16:
+// for each 16-column block: wave 0 factors the 16x16 diagonal block in registers (lane r holds
+// row r; column broadcasts by v_readlane) and inverts it (lane c solves for column c); all four
+// waves then apply the 16-wide panel solve and the rank-16 trailing update. The inverse of the
+// whole tile is assembled from the 16x16 block inverses, X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb.
 __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, int64_t dstride,
                                                    double* ldet, int64_t lstride, Live live,
                                                    int fail_code) {
     const int b = blockIdx.x;
     if (!chain_live(live, b)) return;
     __shared__ double T[64][65];
-    const int tid = threadIdx.x;
+    __shared__ double Xi[64][65];
+    __shared__ double Tmp[3][16][17];
+    __shared__ int sfail;
+    __shared__ double sld;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     double* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
-    for (int e = tid; e < 4096; e += 256) T[e >> 6][e & 63] = At[(int64_t)(e >> 6) * A.ld + (e & 63)];
+    for (int e = tid; e < 4096; e += 256) {
+        T[e >> 6][e & 63] = At[(int64_t)(e >> 6) * A.ld + (e & 63)];
+        Xi[e >> 6][e & 63] = 0.0;
+    }
+    if (tid == 0) {
+        sfail = 0;
+        sld = 0.0;
+    }
     __syncthreads();
-    double lsum = 0.0;
-    for (int j = 0; j < 64; ++j) {
-        const double p = T[j][j];
-        if (!(p > 0.0)) {  // non-positive or NaN pivot: uniform across the block
+    for (int kb = 0; kb < 4; ++kb) {
+        const int o = kb * 16;
+        if (w == 0) {
+            const int r = lane & 15;
+            double row[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) row[c] = T[o + r][o + c];
+            bool bad = false;
+            double lsum = 0.0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const double p = rdlane(row[j], j);
+                bad |= !(p > 0.0);
+                const double d = sqrt(p);
+                const double invd = 1.0 / d;
+                lsum += log(d);
+                if (r > j) row[j] *= invd;
+                if (r == j) row[j] = d;
+#pragma unroll
+                for (int c = j + 1; c < 16; ++c) row[c] -= row[j] * rdlane(row[j], c);
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) T[o + r][o + c] = (c <= r) ? row[c] : 0.0;
+            }
+            // lane c (< 16): column c of inv(L_bb) by forward substitution
+            const int c = lane & 15;
+            double x[16];
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                double s = (rr == c) ? 1.0 : 0.0;
+#pragma unroll
+                for (int m = 0; m < rr; ++m) s -= rdlane(row[m], rr) * x[m];
+                x[rr] = (rr >= c) ? s / rdlane(row[rr], rr) : 0.0;
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) Xi[o + rr][o + c] = x[rr];
+            }
+            if (lane == 0) {
+                if (bad) sfail = 1;
+                sld += lsum;
+            }
+        }
+        __syncthreads();
+        if (sfail) {
             if (tid == 0) live.status[b] = fail_code;
             return;
         }
-        const double d = sqrt(p);
-        const double invd = 1.0 / d;
-        lsum += log(d);
-        if (tid > j && tid < 64) T[tid][j] *= invd;
-        __syncthreads();
-        const int m = 63 - j;
-        for (int e = tid; e < m * m; e += 256) {
-            const int r = j + 1 + e / m, c = j + 1 + e % m;
-            if (c <= r) T[r][c] -= T[r][j] * T[c][j];
+        if (kb == 3) break;
+        // panel: T[i][c] = sum_{m=o}^{c} T[i][m] * inv[c][m],  i in [o+16, 64), c in [o, o+16)
+        const int nel = (48 - o) * 16;
+        double pv[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int e = tid + q * 256;
+            pv[q] = 0.0;
+            if (e < nel) {
+                const int i = o + 16 + (e >> 4), c = o + (e & 15);
+                double s = 0.0;
+                for (int m = o; m <= c; ++m) s += T[i][m] * Xi[c][m];
+                pv[q] = s;
+            }
         }
-        if (tid == 0) T[j][j] = d;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int e = tid + q * 256;
+            if (e < nel) T[o + 16 + (e >> 4)][o + (e & 15)] = pv[q];
+        }
+        __syncthreads();
+        // rank-16 trailing update of the lower part of T[o+16:, o+16:]
+        const int m0 = o + 16, sz = 64 - m0;
+        for (int e = tid; e < sz * sz; e += 256) {
+            const int i = m0 + e / sz, j = m0 + e % sz;
+            if (j <= i) {
+                double s = T[i][j];
+#pragma unroll
+                for (int m = 0; m < 16; ++m) s -= T[i][o + m] * T[j][o + m];
+                T[i][j] = s;
+            }
+        }
         __syncthreads();
     }
-    // write L_kk (lower; the strict upper part of the diagonal tile is zeroed)
+    // off-diagonal blocks of the inverse, block row by block row
+    for (int a = 1; a < 4; ++a) {
+        // Tmp[b'] = sum_{kk=b'}^{a-1} L_{a,kk} X_{kk,b'}   for b' < a
+        for (int e = tid; e < a * 256; e += 256) {
+            const int bb = e >> 8, r = (e >> 4) & 15, c = e & 15;
+            double s = 0.0;
+            for (int m = bb * 16; m < a * 16; ++m) s += T[a * 16 + r][m] * Xi[m][bb * 16 + c];
+            Tmp[bb][r][c] = s;
+        }
+        __syncthreads();
+        // X_{a,b'} = -X_aa Tmp[b']
+        for (int e = tid; e < a * 256; e += 256) {
+            const int bb = e >> 8, r = (e >> 4) & 15, c = e & 15;
+            double s = 0.0;
+            for (int m = 0; m <= r; ++m) s -= Xi[a * 16 + r][a * 16 + m] * Tmp[bb][m][c];
+            Xi[a * 16 + r][bb * 16 + c] = s;
+        }
+        __syncthreads();
+    }
+    double* D = Dinv + b * dstride + (int64_t)k * 4096;
     for (int e = tid; e < 4096; e += 256) {
         const int r = e >> 6, c = e & 63;
         At[(int64_t)r * A.ld + c] = (c <= r) ? T[r][c] : 0.0;
+        D[e] = Xi[r][c];
     }
-    if (tid == 0) ldet[b * lstride + k] = lsum;
-    // inverse: lane c computes column c of inv(L) by forward substitution
-    if (tid < 64) {
-        const int c = tid;
-        double x[64];
-#pragma unroll
-        for (int r = 0; r < 64; ++r) {
-            double s = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-            for (int m = 0; m < r; ++m) s -= T[r][m] * x[m];
-            x[r] = (r >= c) ? s / T[r][r] : 0.0;
-        }
-        double* D = Dinv + b * dstride + (int64_t)k * 4096;
-#pragma unroll
-        for (int r = 0; r < 64; ++r) D[r * 64 + c] = x[r];
-    }
+    if (tid == 0) ldet[b * lstride + k] = sld;
 }
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
@@ -170,64 +263,65 @@ void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t
 }
 
 // ------------------------------------------------------------------------------- trailing update
-// Tiles (i, j) with i in [i0, R), k < j <= min(i, Cb-1), enumerated as a triangular part (rows
-// i < Cb, i-k tiles each) followed by a rectangular part (rows i >= Cb, Cb-1-k tiles each).
-__device__ __forceinline__ void decode_update_tile(long t, int k, int i0, int R, int Cb, int& i,
+// A_ij -= sum_{q<kc} A_{i,k0+q} A_{j,k0+q}^T for tiles i in [i0, R), j in [j0, min(i, jend-1)]
+// (i0 >= j0). Enumerated as a triangular part (rows i < jend: i-j0+1 tiles) followed by a
+// rectangular part (rows i >= jend: jend-j0 tiles).
+__device__ __forceinline__ void decode_update_tile(long t, int i0, int R, int j0, int jend, int& i,
                                                    int& j) {
-    const int it_end = min(R, Cb);
-    const int a0 = i0 - k;  // tiles in the first triangular row
-    const int ntri_rows = max(0, it_end - i0);
+    const int a0 = i0 - j0 + 1;
+    const int ntri_rows = max(0, min(R, jend) - i0);
     const long ntri = (long)ntri_rows * a0 + (long)ntri_rows * (ntri_rows - 1) / 2;
     if (t < ntri) {
-        // largest p with p*a0 + p(p-1)/2 <= t
         const double aa = a0 - 0.5;
         long p = (long)floor(-aa + sqrt(aa * aa + 2.0 * (double)t));
         while (p > 0 && p * a0 + p * (p - 1) / 2 > t) --p;
         while ((p + 1) * a0 + (p + 1) * p / 2 <= t) ++p;
         i = i0 + (int)p;
-        j = k + 1 + (int)(t - (p * a0 + p * (p - 1) / 2));
+        j = j0 + (int)(t - (p * a0 + p * (p - 1) / 2));
     } else {
         const long r = t - ntri;
-        const int w = Cb - 1 - k;
-        i = max(i0, Cb) + (int)(r / w);
-        j = k + 1 + (int)(r % w);
+        const int wdt = jend - j0;
+        i = max(i0, jend) + (int)(r / wdt);
+        j = j0 + (int)(r % wdt);
     }
 }
 
-static long update_tile_count(int k, int i0, int R, int Cb) {
-    const int it_end = R < Cb ? R : Cb;
-    const int ntri_rows = it_end - i0 > 0 ? it_end - i0 : 0;
-    const long a0 = i0 - k;
+long update_tile_count(int i0, int R, int j0, int jend) {
+    if (jend <= j0 || R <= i0) return 0;
+    const long a0 = i0 - j0 + 1;
+    const int ntri_rows = std::max(0, std::min(R, jend) - i0);
     long n = ntri_rows * a0 + (long)ntri_rows * (ntri_rows - 1) / 2;
-    const int rect_rows = R - (i0 > Cb ? i0 : Cb);
-    if (rect_rows > 0) n += (long)rect_rows * (Cb - 1 - k);
+    const int rect_rows = R - std::max(i0, jend);
+    if (rect_rows > 0) n += (long)rect_rows * (jend - j0);
     return n;
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(MatB A, int k, int i0, int R, int Cb,
-                                                     Live live) {
+__global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc, int i0, int R,
+                                                     int j0, int jend, Live live) {
     const int b = blockIdx.y;
     if (!chain_live(live, b)) return;
     int i, j;
-    decode_update_tile(blockIdx.x, k, i0, R, Cb, i, j);
+    decode_update_tile(blockIdx.x, i0, R, j0, jend, i, j);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
     double* Ab = A.base + b * A.cstride;
     double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
-    const double* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
-    const double* Ajk = Ab + (int64_t)(j * 64) * A.ld + k * 64;
     d4_t acc[2][2];
     tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
-    tile_nt_f64<true>(acc, Aik, A.ld, Ajk, A.ld, wr, wc, lane);
+    for (int q = 0; q < kc; ++q) {
+        const double* Aik = Ab + (int64_t)(i * 64) * A.ld + (k0 + q) * 64;
+        const double* Ajk = Ab + (int64_t)(j * 64) * A.ld + (k0 + q) * 64;
+        tile_nt_f64<true>(acc, Aik, A.ld, Ajk, A.ld, wr, wc, lane);
+    }
     tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
 }
 
-void launch_chol_update(MatB A, int k, int i0, int R, int Cb, Live live, int nchains,
-                        hipStream_t s) {
-    if (i0 < k + 1) i0 = k + 1;
-    const long n = update_tile_count(k, i0, R, Cb);
+void launch_chol_update(MatB A, int k0, int kc, int i0, int R, int j0, int jend, Live live,
+                        int nchains, hipStream_t s) {
+    if (i0 < j0) i0 = j0;
+    const long n = update_tile_count(i0, R, j0, jend);
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)n, nchains), dim3(256), 0, s, A, k, i0, R,
-                       Cb, live);
+    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)n, nchains), dim3(256), 0, s, A, k0, kc, i0,
+                       R, j0, jend, live);
 }
 
 // ------------------------------------------------------------------------------- L^T z = r
