@@ -79,11 +79,78 @@ __device__ __forceinline__ void tile_acc_store(const d4_t (&acc)[2][2], double* 
                   (lane & 15)] = acc[bi][bj][r];
 }
 
+// acc += (NEG ? -1 : 1) * A[64 x 16*nsub] * B[64 x 16*nsub]^T for the workgroup's 64x64 tile.
+// Operands are staged through LDS in 16-deep slices shared by the four waves (half the L2
+// traffic of per-wave loads), double-buffered: the global loads of slice s+1 are in flight
+// while the MFMAs of slice s run; one barrier per slice. LDS pitch 17 doubles makes the
+// fragment reads (16 rows x 2 k per 32-lane group) bank-conflict free for ds_read_b64.
+#define KSUB 16
+#define LPITCH 17
+struct GemmSmem {
+    double a[2][64][LPITCH];
+    double b[2][64][LPITCH];
+};
+
+template <bool NEG>
+__device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __restrict__ A,
+                                             int64_t lda, const double* __restrict__ B,
+                                             int64_t ldb, int nsub, GemmSmem& sm) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    // staging map: 512 pieces of 16 B per operand slice (64 rows x 128 B); thread -> pieces
+    // tid and tid+256: row = p >> 3, col = (p & 7) * 2
+    const int pr0 = tid >> 3, pc = (tid & 7) * 2, pr1 = pr0 + 32;
+    d2_t ra0, ra1, rb0, rb1;
+    auto gload = [&](int sidx) {
+        const int kc = sidx * KSUB + pc;
+        ra0 = *reinterpret_cast<const d2_t*>(A + (int64_t)pr0 * lda + kc);
+        ra1 = *reinterpret_cast<const d2_t*>(A + (int64_t)pr1 * lda + kc);
+        rb0 = *reinterpret_cast<const d2_t*>(B + (int64_t)pr0 * ldb + kc);
+        rb1 = *reinterpret_cast<const d2_t*>(B + (int64_t)pr1 * ldb + kc);
+    };
+    auto sstore = [&](int buf) {
+        sm.a[buf][pr0][pc] = NEG ? -ra0.x : ra0.x;
+        sm.a[buf][pr0][pc + 1] = NEG ? -ra0.y : ra0.y;
+        sm.a[buf][pr1][pc] = NEG ? -ra1.x : ra1.x;
+        sm.a[buf][pr1][pc + 1] = NEG ? -ra1.y : ra1.y;
+        sm.b[buf][pr0][pc] = rb0.x;
+        sm.b[buf][pr0][pc + 1] = rb0.y;
+        sm.b[buf][pr1][pc] = rb1.x;
+        sm.b[buf][pr1][pc + 1] = rb1.y;
+    };
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int s = 0; s < nsub; ++s) {
+        const int cur = s & 1;
+        if (s + 1 < nsub) gload(s + 1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            double a[2], b[2];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) a[bi] = sm.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) b[bj] = sm.b[cur][32 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+                    acc[bi][bj] =
+                        __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi], b[bj], acc[bi][bj], 0, 0, 0);
+        }
+        if (s + 1 < nsub) sstore(cur ^ 1);
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
     return lv.active[b] != 0 && lv.status[b] == 0;
 }
 
 // ------------------------------------------------------------------------------- diagonal tile
+#ifdef APM_DIAG_STAMPS
+__device__ unsigned long long g_diag_stamps[16];  // diagnostic build only (tools/diag_stamps.cpp)
+#endif
 // Broadcast lane l's value of a wave-uniform-indexed register (v_readlane x2).
 __device__ __forceinline__ double rdlane(double v, int l) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -106,17 +173,22 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, 
     __shared__ double Xi[64][65];
     __shared__ double Tmp[3][16][17];
     __shared__ int sfail;
-    __shared__ double sld;
+    __shared__ double sdg[64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#ifdef APM_DIAG_STAMPS
+    unsigned long long stamps[16];
+    int ns = 0;
+#define STAMP() if (tid == 0 && ns < 16) stamps[ns++] = __builtin_amdgcn_s_memtime()
+#else
+#define STAMP()
+#endif
+    STAMP();
     double* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
     for (int e = tid; e < 4096; e += 256) {
         T[e >> 6][e & 63] = At[(int64_t)(e >> 6) * A.ld + (e & 63)];
         Xi[e >> 6][e & 63] = 0.0;
     }
-    if (tid == 0) {
-        sfail = 0;
-        sld = 0.0;
-    }
+    if (tid == 0) sfail = 0;
     __syncthreads();
     for (int kb = 0; kb < 4; ++kb) {
         const int o = kb * 16;
@@ -126,16 +198,18 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, 
 #pragma unroll
             for (int c = 0; c < 16; ++c) row[c] = T[o + r][o + c];
             bool bad = false;
-            double lsum = 0.0;
+            double rinv[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const double p = rdlane(row[j], j);
                 bad |= !(p > 0.0);
-                const double d = sqrt(p);
-                const double invd = 1.0 / d;
-                lsum += log(d);
-                if (r > j) row[j] *= invd;
-                if (r == j) row[j] = d;
+                // 1/sqrt(p) by v_rsq_f64 + two Newton steps; d = p / sqrt(p)
+                double yv = __builtin_amdgcn_rsq(p);
+                yv = yv * (1.5 - 0.5 * p * yv * yv);
+                yv = yv * (1.5 - 0.5 * p * yv * yv);
+                const double d = p * yv;
+                rinv[j] = yv;
+                row[j] = (r > j) ? row[j] * yv : ((r == j) ? d : row[j]);
 #pragma unroll
                 for (int c = j + 1; c < 16; ++c) row[c] -= row[j] * rdlane(row[j], c);
             }
@@ -151,18 +225,17 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, 
                 double s = (rr == c) ? 1.0 : 0.0;
 #pragma unroll
                 for (int m = 0; m < rr; ++m) s -= rdlane(row[m], rr) * x[m];
-                x[rr] = (rr >= c) ? s / rdlane(row[rr], rr) : 0.0;
+                x[rr] = (rr >= c) ? s * rinv[rr] : 0.0;
             }
             if (lane < 16) {
 #pragma unroll
                 for (int rr = 0; rr < 16; ++rr) Xi[o + rr][o + c] = x[rr];
             }
-            if (lane == 0) {
-                if (bad) sfail = 1;
-                sld += lsum;
-            }
+            if (lane < 16) sdg[o + lane] = row[lane];  // lane r: L[r][r] sits in row[r]
+            if (lane == 0 && bad) sfail = 1;
         }
         __syncthreads();
+        STAMP();
         if (sfail) {
             if (tid == 0) live.status[b] = fail_code;
             return;
@@ -201,6 +274,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, 
             }
         }
         __syncthreads();
+        STAMP();
     }
     // off-diagonal blocks of the inverse, block row by block row
     for (int a = 1; a < 4; ++a) {
@@ -221,13 +295,22 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, 
         }
         __syncthreads();
     }
+    STAMP();
     double* D = Dinv + b * dstride + (int64_t)k * 4096;
     for (int e = tid; e < 4096; e += 256) {
         const int r = e >> 6, c = e & 63;
         At[(int64_t)r * A.ld + c] = (c <= r) ? T[r][c] : 0.0;
         D[e] = Xi[r][c];
     }
-    if (tid == 0) ldet[b * lstride + k] = sld;
+    if (w == 0) {  // sum of log L_ii, one lane per pivot
+        const double l = wave_sum_d(log(sdg[lane]));
+        if (lane == 0) ldet[b * lstride + k] = l;
+    }
+#ifdef APM_DIAG_STAMPS
+    STAMP();
+    if (tid == 0 && k == 0 && b == 0)
+        for (int q = 0; q < ns; ++q) g_diag_stamps[q] = stamps[q] - stamps[0];
+#endif
 }
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
@@ -245,14 +328,14 @@ __global__ __launch_bounds__(256) void k_chol_panel(MatB A, int k, int i0, const
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
     double* At = A.base + b * A.cstride + (int64_t)(i * 64) * A.ld + k * 64;
     const double* D = Dinv + b * dstride + (int64_t)k * 4096;
+    __shared__ GemmSmem sm;
     d4_t acc[2][2];
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
-    tile_nt_f64<false>(acc, At, A.ld, D, 64, wr, wc, lane);  // X = A_ik * inv(L_kk)^T
-    __syncthreads();  // every wave has read A_ik before it is overwritten
-    tile_acc_store(acc, At, A.ld, wr, wc, lane);
+    tile_gemm_nt<false>(acc, At, A.ld, D, 64, 4, sm);  // X = A_ik * inv(L_kk)^T
+    tile_acc_store(acc, At, A.ld, wr, wc, lane);  // A_ik fully staged before the last barrier
 }
 
 void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
@@ -305,13 +388,11 @@ __global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc, int
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
     double* Ab = A.base + b * A.cstride;
     double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
+    __shared__ GemmSmem sm;
     d4_t acc[2][2];
     tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
-    for (int q = 0; q < kc; ++q) {
-        const double* Aik = Ab + (int64_t)(i * 64) * A.ld + (k0 + q) * 64;
-        const double* Ajk = Ab + (int64_t)(j * 64) * A.ld + (k0 + q) * 64;
-        tile_nt_f64<true>(acc, Aik, A.ld, Ajk, A.ld, wr, wc, lane);
-    }
+    tile_gemm_nt<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
+                       Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 4 * kc, sm);
     tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
 }
 
@@ -373,9 +454,10 @@ void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_
 __global__ __launch_bounds__(256) void k_tile_nt_test(const double* A, const double* B,
                                                       double* C) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+    __shared__ GemmSmem sm;
     d4_t acc[2][2];
     tile_acc_load(acc, C, 64, wr, wc, lane);
-    tile_nt_f64<false>(acc, A, 64, B, 64, wr, wc, lane);
+    tile_gemm_nt<false>(acc, A, 64, B, 64, 4, sm);
     tile_acc_store(acc, C, 64, wr, wc, lane);
 }
 
