@@ -1,0 +1,237 @@
+# -*- coding: utf-8 -*-
+"""Many independent APM chains advanced in lockstep on one MI355X.
+
+``BatchedAPMEllSSPlusRandDirSliceSampler`` runs ``n_chains`` copies of the reference's
+``APMEllSSPlusRandDirSliceSampler`` transition (elliptical slice sampling on the auxiliary
+draws u, random-direction linear slice sampling on theta; reference samplers.py:1007-1089 with
+mcmc_updates.py:311-400, :403-519) as masked lockstep rounds: every shrink iteration of every
+still-undecided chain is one batched estimator call, so the device always sees a batch.
+
+Per chain the control flow, the cache protocol and the host-RNG draw order are those of the
+reference (one ``numpy.random.RandomState`` per chain for the slice heights, angles, offsets and
+directions). The auxiliary draws u and nu live on the device: they are produced by Philox4x32-10
+(one counter stream per chain) and the E-SS proposal u cos(phi) + nu sin(phi) is formed on the
+device, so trajectories are statistically — not bitwise — equivalent to a numpy-u_sampler run
+(DESIGN.md §6). The log target is estimator + log-Gamma prior (E-SS+RD-SS.ipynb:167-173), the
+tau prior applied to every ARD length-scale (gpdemo.utils.log_prior_ard).
+"""
+import warnings
+
+import numpy as np
+
+from gpdemo import _native
+from gpdemo.utils import log_prior_ard
+
+__all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler']
+
+_EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC}
+
+
+class BatchedAPMEllSSPlusRandDirSliceSampler(object):
+    """Lockstep batch of APM E-SS(u) + RD-SS(theta) chains on one device.
+
+    Parameters mirror the notebook protocol: ``kernel`` 'ard' | 'iso', ``epsilon`` jitter,
+    ``n_imp`` importance samples, slice width ``w`` and ``max_steps_out`` (E-SS+RD-SS.ipynb:64-67),
+    ``prior`` the log-Gamma hyper-parameters (a_sigma, b_sigma, a_tau, b_tau).
+    """
+
+    def __init__(self, X, y, n_chains, n_imp, prior, kernel='ard', epsilon=1e-8, w=1.,
+                 max_steps_out=0, max_slice_iters=1000, seed=0, estimator='is', device=None):
+        self.n_chains = int(n_chains)
+        self.n_imp = int(n_imp)
+        self.prior = dict(prior)
+        self.w = float(w)
+        self.max_steps_out = int(max_steps_out)
+        self.max_slice_iters = int(max_slice_iters)
+        self.est = _EST[estimator]
+        kind = _native.KERNEL_ARD if kernel == 'ard' else _native.KERNEL_ISO
+        C = self.n_chains
+        self.ctx = _native.Context(X, y, kind, epsilon, n_imp, max_batch=C, n_slots=2 * C,
+                                   n_ubufs=3 * C, device=device)
+        self.P = self.ctx.theta_len
+        self.slot_cur = np.arange(C, dtype=np.int64)
+        self.slot_prop = np.arange(C, 2 * C, dtype=np.int64)
+        self.ub_u = np.arange(C, dtype=np.int64)
+        self.ub_nu = np.arange(C, 2 * C, dtype=np.int64)
+        self.ub_prop = np.arange(2 * C, 3 * C, dtype=np.int64)
+        ss = np.random.SeedSequence(seed)
+        kids = ss.spawn(C)
+        self.prngs = [np.random.RandomState(np.random.MT19937(k)) for k in kids]
+        self.dev_seeds = np.array([k.generate_state(2, np.uint64)[0] for k in kids],
+                                  dtype=np.uint64)
+        self.dev_ctr = np.zeros(C, dtype=np.uint64)
+        self.theta = np.zeros((C, self.P))
+        self.log_f = np.full(C, -np.inf)
+        self.failed = np.zeros(C, dtype=bool)
+        self.fail_status = np.zeros(C, dtype=np.int32)
+        self.n_theta_calls = 0
+        self.n_u_calls = 0
+        self.n_cubic_ops = np.zeros(C, dtype=np.int64)
+
+    # ------------------------------------------------------------------ helpers
+    def log_prior(self, thetas):
+        return np.array([log_prior_ard(t, self.prior) for t in np.atleast_2d(thetas)])
+
+    def _normals(self, idx, bufs):
+        self.ctx.u_normal(bufs[idx], self.dev_seeds[idx], self.dev_ctr[idx])
+        self.dev_ctr[idx] += 1
+
+    def _theta_eval(self, idx, thetas, slots):
+        out, st, nops = self.ctx.theta_eval(self.est, thetas, self.ub_u[idx], slots)
+        self.n_theta_calls += len(idx)
+        self.n_cubic_ops[idx] += nops
+        bad = st != 0
+        if bad.any():
+            self.failed[idx[bad]] = True
+            self.fail_status[idx[bad]] = st[bad]
+            out = np.where(bad, -np.inf, out)
+        return out + self.log_prior(thetas)
+
+    def prior_draw(self):
+        """theta_init ~ prior per chain, drawn with each chain's RandomState
+        (E-SS+RD-SS.ipynb:198-201, extended to every ARD length-scale)."""
+        th = np.empty((self.n_chains, self.P))
+        for c, rng in enumerate(self.prngs):
+            th[c, 0] = np.log(rng.gamma(self.prior['a_sigma'], 1. / self.prior['b_sigma']))
+            th[c, 1:] = np.log(rng.gamma(self.prior['a_tau'], 1. / self.prior['b_tau'],
+                                         size=self.P - 1))
+        return th
+
+    def initialise(self, theta_init=None):
+        """u ~ N(0, I) on the device and the first theta-call (reference samplers.py:825-827)."""
+        idx = np.arange(self.n_chains)
+        self.theta = self.prior_draw() if theta_init is None else np.array(theta_init, float)
+        self._normals(idx, self.ub_u)
+        self.log_f = self._theta_eval(idx, self.theta, self.slot_cur[idx])
+        return self.theta.copy()
+
+    # ------------------------------------------------------------------ updates
+    def _ess_u(self):
+        """Elliptical slice update of every live chain's u (mcmc_updates.py:372-400)."""
+        live = np.flatnonzero(~self.failed)
+        if live.size == 0:
+            return
+        self._normals(live, self.ub_nu)
+        log_y = np.empty(self.n_chains)
+        phi = np.empty(self.n_chains)
+        lo = np.empty(self.n_chains)
+        hi = np.empty(self.n_chains)
+        for c in live:
+            rng = self.prngs[c]
+            log_y[c] = self.log_f[c] + np.log(rng.uniform())
+            phi[c] = rng.uniform() * 2. * np.pi
+            lo[c], hi[c] = phi[c] - 2. * np.pi, phi[c]
+        act = live
+        it = 0
+        while act.size:
+            if it >= self.max_slice_iters:
+                self.failed[act] = True
+                break
+            self.ctx.u_combine(self.ub_prop[act], self.ub_u[act], self.ub_nu[act],
+                               np.cos(phi[act]), np.sin(phi[act]))
+            out, st = self.ctx.u_eval(self.slot_cur[act], self.ub_prop[act])
+            self.n_u_calls += act.size
+            lf = np.where(st == 0, out, -np.inf) + self.log_prior(self.theta[act])
+            keep = []
+            for q, c in enumerate(act):
+                if lf[q] > log_y[c]:
+                    self.ub_u[c], self.ub_prop[c] = self.ub_prop[c], self.ub_u[c]
+                    self.log_f[c] = lf[q]
+                    continue
+                if phi[c] < 0:
+                    lo[c] = phi[c]
+                elif phi[c] > 0:
+                    hi[c] = phi[c]
+                else:
+                    warnings.warn('Slice collapsed to current value')
+                    continue
+                phi[c] = lo[c] + self.prngs[c].uniform() * (hi[c] - lo[c])
+                keep.append(c)
+            act = np.array(keep, dtype=np.int64)
+            it += 1
+
+    def _rdss_theta(self):
+        """Random-direction linear slice update of every live chain's theta
+        (samplers.py:1071-1089 over mcmc_updates.py:480-519)."""
+        live = np.flatnonzero(~self.failed)
+        if live.size == 0:
+            return
+        C = self.n_chains
+        d = np.zeros((C, self.P))
+        log_y = np.empty(C)
+        x_lo = np.empty(C)
+        x_hi = np.empty(C)
+        for c in live:
+            rng = self.prngs[c]
+            dd = rng.normal(size=self.P)
+            d[c] = dd / dd.dot(dd) ** 0.5
+            log_y[c] = np.log(rng.uniform()) + self.log_f[c]
+            x_lo[c] = 0. - self.w * rng.uniform()
+            x_hi[c] = x_lo[c] + self.w
+        if self.max_steps_out > 0:
+            self._step_out(live, d, log_y, x_lo, x_hi)
+        x_prop = np.empty(C)
+        act = live[~self.failed[live]]
+        it = 0
+        while act.size:
+            if it >= self.max_slice_iters:
+                self.failed[act] = True
+                break
+            for c in act:
+                x_prop[c] = x_lo[c] + (x_hi[c] - x_lo[c]) * self.prngs[c].uniform()
+            th_p = self.theta[act] + x_prop[act, None] * d[act]
+            lf = self._theta_eval(act, th_p, self.slot_prop[act])
+            keep = []
+            for q, c in enumerate(act):
+                if lf[q] > log_y[c]:
+                    # the accepted call's cache becomes the current one (samplers.py:1079-1086)
+                    self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
+                    self.theta[c] = th_p[q]
+                    self.log_f[c] = lf[q]
+                    continue
+                if self.failed[c]:
+                    continue
+                if x_prop[c] < 0.:
+                    x_lo[c] = x_prop[c]
+                elif x_prop[c] > 0.:
+                    x_hi[c] = x_prop[c]
+                else:
+                    warnings.warn('Slice collapsed to current value')
+                    continue
+                keep.append(c)
+            act = np.array(keep, dtype=np.int64)
+            it += 1
+
+    def _step_out(self, live, d, log_y, x_lo, x_hi):
+        """Stepping out (mcmc_updates.py:486-498): split max_steps_out at random, extend each
+        end by w while it is inside the slice. Every probe is a theta-call."""
+        C = self.n_chains
+        down = np.zeros(C)
+        up = np.zeros(C)
+        for c in live:
+            down[c] = np.round(self.prngs[c].uniform() * self.max_steps_out)
+            up[c] = self.max_steps_out - down[c]
+        for ends, budget, sign in ((x_lo, down, -1.), (x_hi, up, 1.)):
+            s = np.zeros(C)
+            act = live[(s[live] < budget[live]) & ~self.failed[live]]
+            while act.size:
+                lf = self._theta_eval(act, self.theta[act] + ends[act, None] * d[act],
+                                      self.slot_prop[act])
+                inside = log_y[act] < lf
+                grow = act[inside]
+                ends[grow] += sign * self.w
+                s[grow] += 1
+                act = grow[s[grow] < budget[grow]]
+
+    def step(self):
+        """One transition (u then theta) of every live chain; returns thetas (n_chains, P)."""
+        self._ess_u()
+        self._rdss_theta()
+        return self.theta.copy()
+
+    def run(self, n_steps, theta_init=None, warmup_callback=None):
+        thetas = np.empty((self.n_chains, n_steps, self.P))
+        thetas[:, 0] = self.initialise(theta_init)
+        for s in range(1, n_steps):
+            thetas[:, s] = self.step()
+        return thetas

@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: MCMC iters/s + ESS/s on theta, GP classification N=4096,
+N_imp=256, on 1/2/4/8 MI355X (one process per GPU, chains sharded, no collective on the data path).
+
+Workload (BASELINE.json configs[3]/[2]): synthetic probit GP-classification data (N=4096, D=32,
+ARD squared-exponential kernel), APM with elliptical-slice updates of u and random-direction
+slice updates of theta (E-SS+RD-SS.ipynb protocol, w=1, max_steps_out=0), ApproxPosteriorIS
+estimator with N_imp=256, `--chains` independent chains per GPU advanced in lockstep.
+A step = one MCMC transition (u-update + theta-update) of every chain on every GPU.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints one JSON line (contract in the task statement); `roofline` is the dominant kernel
+(the f64-MFMA Cholesky trailing update) timed with HIP events on the context's stream over the
+timed region; `cpu_baseline` times the CPU restatement of the reference (oracle/) on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'auxiliary-pm-mcmc_amd'))
+
+METRIC = BASE_METRIC = 'MCMC iters/sec + ESS/sec on θ, GP-classif N=4096 N_imp=256, 1/2/4/8 GPU'
+PEAK_F64_MFMA_TFLOPS = 78.6   # MI355X FP64 matrix, spec (not in MI355X_MICROARCH.md)
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_*_f32)
+PEAK_HBM_TBS = 8.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--chains', type=int, default=64, help='chains per GPU')
+    ap.add_argument('--n', type=int, default=4096)
+    ap.add_argument('--d', type=int, default=32)
+    ap.add_argument('--n-imp', type=int, default=256)
+    ap.add_argument('--seed', type=int, default=20151009)
+    ap.add_argument('--cpu-baseline', type=int, default=1)
+    ap.add_argument('--cpu-budget', type=float, default=30.0,
+                    help='approximate seconds of CPU work for the baseline sample')
+    return ap.parse_args()
+
+
+class Dist(object):
+    """One process per GPU. torch.distributed only for the barrier and the max/sum reductions of
+    the timing (RCCL on GPUs, gloo for CPU tests); the chains never exchange data."""
+
+    def __init__(self, backend=None):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend is None:
+                backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+            if backend == 'nccl':
+                torch.cuda.set_device(self.local_rank)
+            dist.init_process_group(backend=backend)
+            self.dist = dist
+            self.backend = backend
+
+    def _t(self, x):
+        import torch
+        dev = 'cuda' if self.backend == 'nccl' else 'cpu'
+        return torch.tensor([float(x)], dtype=torch.float64, device=dev)
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.dist is None:
+            return float(x)
+        t = self._t(x)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if self.dist is None:
+            return float(x)
+        t = self._t(x)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def device_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def timed_region(dist, step_fn, steps):
+    """barrier + sync, K steps, barrier + sync; returns the max over ranks of the wall time."""
+    dist.barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step_fn()
+    device_sync()
+    dist.barrier()
+    return dist.max(time.perf_counter() - t0)
+
+
+def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget):
+    """Time the CPU restatement (oracle/: C Gram + scipy LAPACK, the reference's op order) on a
+    bounded sample: theta-calls and cached u-calls at the benchmark size, composed into
+    transitions/s with the per-transition call counts measured on the GPU run."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import apm_oracle as orc
+    try:
+        from threadpoolctl import threadpool_info
+        blas_threads = max([i.get('num_threads', 1) for i in threadpool_info()
+                            if i.get('user_api') == 'blas'] or [1])
+    except Exception:
+        blas_threads = None
+    est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
+    rng = np.random.RandomState(0)
+    ns = rng.normal(size=(X.shape[0], n_imp))
+    t_theta, t_u = [], []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        _, cache = est(ns, theta)
+        t1 = time.perf_counter()
+        est(ns, None, cache)
+        t2 = time.perf_counter()
+        t_theta.append(t1 - t0)
+        t_u.append(t2 - t1)
+        if time.perf_counter() - t_start > 0.5 * budget or len(t_theta) >= 5:
+            break
+    tt, tu = float(np.median(t_theta)), float(np.median(t_u))
+    per_transition = calls_theta * tt + calls_u * tu
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    return {
+        'value': 1.0 / per_transition, 'unit': 'transitions/s (1 chain)',
+        'cores': blas_threads if blas_threads else cores, 'kind': 'port',
+        'sample': ('{0} theta-call(s) {1:.2f} s and cached u-call(s) {2:.3f} s (median) of the '
+                   'oracle ApproxPosteriorIS (C Gram 1 thread + scipy/OpenBLAS {3} threads, {4} '
+                   'cores visible) at N={5} D={6} N_imp={7}, composed with {8:.2f} theta-calls + '
+                   '{9:.2f} u-calls per transition measured on the GPU run'
+                   .format(len(t_theta), tt, tu, blas_threads, cores, X.shape[0], X.shape[1],
+                           n_imp, calls_theta, calls_u)),
+        'theta_call_s': tt, 'u_call_s': tu,
+    }
+
+
+def main():
+    a = parse()
+    dist = Dist()
+    from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
+    from auxpm.diagnostics import effective_size
+    from gpdemo import _native
+    from gpdemo.utils import synthetic_gp_data
+
+    X, y = synthetic_gp_data(a.n, a.d, a.seed)
+    prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    smp = BatchedAPMEllSSPlusRandDirSliceSampler(
+        X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
+        seed=a.seed + 7919 * dist.rank, device=dist.local_rank)
+    P = smp.P
+    smp.initialise()
+    for _ in range(a.warmup):
+        smp.step()
+    ctx = smp.ctx
+    for k in (0, 1, 2):
+        ctx.prof_read(k, reset=True)
+    ctx.prof_enable(True)
+    thetas = []
+    th0, u0 = smp.n_theta_calls, smp.n_u_calls
+
+    def one_step():
+        thetas.append(smp.step())
+
+    elapsed = timed_region(dist, one_step, a.steps)
+    ctx.prof_enable(False)
+    live = int((~smp.failed).sum())
+    transitions = dist.sum(live * a.steps)
+    value = transitions / elapsed
+    n_th = (smp.n_theta_calls - th0) / max(1, a.chains * a.steps)
+    n_u = (smp.n_u_calls - u0) / max(1, a.chains * a.steps)
+
+    prof = {}
+    for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm')):
+        prof[name] = ctx.prof_read(k, reset=False)
+    ctx.prof_read(0, reset=True)
+    ms, cnt, flops = prof['chol_update']
+    avg_s = ms * 1e-3 / max(cnt, 1)
+    achieved = (flops / max(cnt, 1)) / avg_s / 1e12 if cnt else 0.0
+    roofline = {'kernel': 'k_chol_update (f64 MFMA trailing update, rank-64/256)',
+                'bound': 'mfma', 'achieved': achieved, 'peak': PEAK_F64_MFMA_TFLOPS,
+                'unit': 'TFLOP/s', 'frac': achieved / PEAK_F64_MFMA_TFLOPS, 'traffic': None,
+                'launches': cnt, 'avg_launch_us': avg_s * 1e6,
+                'algorithmic_flops_per_launch': flops / max(cnt, 1),
+                'share_of_step_time': (ms * 1e-3) / elapsed}
+    extra = {}
+    gms, gcnt, gbytes = prof['gram']
+    if gcnt:
+        ach = gbytes / (gms * 1e-3) / 1e12
+        extra['roofline_gram'] = {'bound': 'hbm', 'achieved': ach, 'peak': PEAK_HBM_TBS,
+                                  'unit': 'TB/s', 'frac': ach / PEAK_HBM_TBS, 'traffic': None,
+                                  'launches': gcnt, 'avg_launch_us': gms * 1e3 / gcnt,
+                                  'algorithmic_bytes_per_launch': gbytes / gcnt}
+    ums, ucnt, uflops = prof['ugemm']
+    if ucnt:
+        ach = uflops / (ums * 1e-3) / 1e12
+        extra['roofline_lu'] = {'bound': 'mfma', 'achieved': ach, 'peak': PEAK_F32_MFMA_TFLOPS,
+                                'unit': 'TFLOP/s', 'frac': ach / PEAK_F32_MFMA_TFLOPS,
+                                'traffic': None, 'launches': ucnt,
+                                'avg_launch_us': ums * 1e3 / ucnt,
+                                'algorithmic_flops_per_launch': uflops / ucnt}
+    ess_per_sec = None
+    if a.steps >= 100:
+        tr = np.stack(thetas, 1)  # (chains, steps, P)
+        ess = sum(effective_size(tr[c]).min() for c in range(a.chains) if not smp.failed[c])
+        ess_per_sec = dist.sum(ess) / elapsed
+
+    cpu = None
+    if a.cpu_baseline and dist.rank == 0 and dist.world == 1:
+        theta_ref = np.r_[0.0, np.full(a.d, np.log(np.sqrt(a.d)))]
+        cpu = cpu_baseline(X, y, a.n_imp, theta_ref, n_th, n_u, a.cpu_budget)
+        cpu['value_same_chains'] = cpu['value'] * a.chains
+        cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
+
+    line = {
+        'metric': METRIC, 'value': value, 'unit': 'transitions/s (all chains, all GPUs)',
+        'n_gpus': dist.world, 'steps': a.steps, 'warmup': a.warmup,
+        'ms_per_step': 1e3 * elapsed / a.steps, 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'f64',
+        'dtype_detail': 'theta-path (Gram, Laplace/Newton, Cholesky factors) fp64 on f64 MFMA; '
+                        'importance-sampling L.U fp32 on f32 MFMA; probit/LME epilogue fp32->fp64',
+        'data': 'synthetic (X~N(0,1) normalised, y=sign of a GP prior draw; seed {0})'.format(a.seed),
+        'config': {'workload': 'APM E-SS(u) + RD-SS(theta), ARD-SE probit GP classification, '
+                               'ApproxPosteriorIS estimator (BASELINE.json configs[3], per-GPU '
+                               'share of configs[4])',
+                   'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'n_theta': P,
+                   'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
+                   'parallelism': 'dp{0} (independent chains per GPU, no collective)'
+                   .format(dist.world)},
+        'ess_per_sec': ess_per_sec,
+        'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
+        'failed_chains': int(dist.sum(int(smp.failed.sum()))),
+        'roofline': roofline, 'cpu_baseline': cpu,
+    }
+    line.update(extra)
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+    del _native
+
+
+if __name__ == '__main__':
+    main()
