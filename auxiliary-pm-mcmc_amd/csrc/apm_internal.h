@@ -27,9 +27,12 @@ void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet
                       Live live, int fail_code, int nchains, hipStream_t s);
 void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
                        Live live, int nchains, hipStream_t s);
-void launch_chol_update(MatB A, int k0, int kc, int i0, int R, int j0, int jend, Live live,
+// tiles: device list of packed (i << 16) | j built by build_update_tiles (super-tile order)
+void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                         int nchains, hipStream_t s);
 long update_tile_count(int i0, int R, int j0, int jend);
+#include <vector>
+std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend);
 // one step (block J) of the backward solve L^T z = r, r stored in row `rrow` of A (in place),
 // z written to z[b*zstride + ...]
 void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,

@@ -57,6 +57,8 @@ struct apm_ctx {
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<ProfRec> recs;
+    // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
+    std::map<std::tuple<int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
 };
 
 namespace {
@@ -144,12 +146,25 @@ double update_flops(int i0, int R, int j0, int jend, int kc) {
     return f;
 }
 
+std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend) {
+    auto key = std::make_tuple(i0, R, j0, jend);
+    auto it = c->tile_lists.find(key);
+    if (it != c->tile_lists.end()) return it->second;
+    std::vector<unsigned> v = build_update_tiles(i0, R, j0, jend);
+    unsigned* d = dalloc<unsigned>(c, v.size());
+    HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
+    auto val = std::make_pair(d, (int)v.size());
+    c->tile_lists[key] = val;
+    return val;
+}
+
 void tracked_update(apm_ctx* c, int k0, int kc, int i0, int R, int j0, int jend, int count) {
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
+    const auto tl = tile_list(c, i0, R, j0, jend);
     ProfScope ps(c, APM_PROF_CHOL_UPDATE,
                  c->prof ? update_flops(i0, R, j0, jend, kc) * count : 0.0);
-    launch_chol_update(c->A, k0, kc, i0, R, j0, jend, live_of(c), count, c->stream);
+    launch_chol_update(c->A, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
     check_launch();
 }
 

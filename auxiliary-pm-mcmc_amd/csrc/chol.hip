@@ -6,6 +6,7 @@
 // The work matrix is tiled TB x TB (TB = 64). One workgroup (4 waves) owns one output tile; each
 // wave owns a 32x32 quadrant = 2x2 v_mfma_f64_16x16x4_f64 accumulators.
 #include <algorithm>
+#include <vector>
 
 #include "apm_internal.h"
 
@@ -159,163 +160,178 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-// 64x64 Cholesky + inverse of the lower factor in one workgroup (LDS resident), blocked by 16:
-// for each 16-column block: wave 0 factors the 16x16 diagonal block in registers (lane r holds
-// row r; column broadcasts by v_readlane) and inverts it (lane c solves for column c); all four
-// waves then apply the 16-wide panel solve and the rank-16 trailing update. The inverse of the
-// whole tile is assembled from the 16x16 block inverses, X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb.
-__global__ __launch_bounds__(256) void k_chol_diag(MatB A, int k, double* Dinv, int64_t dstride,
-                                                   double* ldet, int64_t lstride, Live live,
-                                                   int fail_code) {
+// 16x16x16 products on LDS operands with one v_mfma_f64_16x16x4_f64 chain (4 steps):
+//   NT: acc[r][c] += sum_k A[r][k] * B[c][k]      NN: acc[r][c] += sum_k A[r][k] * B[k][c]
+template <bool NEG>
+__device__ __forceinline__ void mm16_nt(d4_t& acc, const double* a, int lda, const double* b,
+                                        int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double av = a[r16 * lda + 4 * t + kq];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -av : av, b[r16 * ldb + 4 * t + kq], acc,
+                                                   0, 0, 0);
+    }
+}
+__device__ __forceinline__ void mm16_nn(d4_t& acc, const double* a, int lda, const double* b,
+                                        int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
+}
+__device__ __forceinline__ void st16(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[((lane >> 4) + 4 * q) * ld + (lane & 15)] = sgn * acc[q];
+}
+__device__ __forceinline__ void ld16(d4_t& acc, const double* src, int ld, int lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = src[((lane >> 4) + 4 * q) * ld + (lane & 15)];
+}
+
+// 64x64 Cholesky + inverse of the lower factor by ONE wave (no barriers), blocked by 16:
+// per 16-column block the 16x16 diagonal block is factored with lane r holding row r in
+// registers (pivot by v_readlane, column broadcast through LDS, 1/sqrt by v_rsq_f64 + two Newton
+// steps) and inverted (lane c substitutes column c); the 16-wide panel solve, the rank-16
+// trailing update and the assembly of the full inverse X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb are
+// 16x16x16 f64-MFMA products on LDS operands.
+#define DP 65
+__global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, int64_t dstride,
+                                                  double* ldet, int64_t lstride, Live live,
+                                                  int fail_code) {
     const int b = blockIdx.x;
     if (!chain_live(live, b)) return;
-    __shared__ double T[64][65];
-    __shared__ double Xi[64][65];
-    __shared__ double Tmp[3][16][17];
-    __shared__ int sfail;
-    __shared__ double sdg[64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ double T[64 * DP];
+    __shared__ double X[64 * DP];
+    __shared__ double Tmp[16 * 17];
+    __shared__ double colb[16];
+    __shared__ double dg[64];
+    const int lane = threadIdx.x;
 #ifdef APM_DIAG_STAMPS
     unsigned long long stamps[16];
     int ns = 0;
-#define STAMP() if (tid == 0 && ns < 16) stamps[ns++] = __builtin_amdgcn_s_memtime()
+#define STAMP() if (lane == 0 && ns < 16) stamps[ns++] = __builtin_amdgcn_s_memtime()
 #else
 #define STAMP()
 #endif
     STAMP();
     double* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
-    for (int e = tid; e < 4096; e += 256) {
-        T[e >> 6][e & 63] = At[(int64_t)(e >> 6) * A.ld + (e & 63)];
-        Xi[e >> 6][e & 63] = 0.0;
+    // 32 KB tile -> LDS: 4 rounds of 8 independent 16-byte loads per lane (lane covers 2 columns)
+#pragma unroll
+    for (int q0 = 0; q0 < 64; q0 += 16) {
+        d2_t v[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const int q = q0 + 2 * h + (lane >> 5);
+            v[h] = *reinterpret_cast<const d2_t*>(At + (int64_t)q * A.ld + 2 * (lane & 31));
+        }
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const int q = q0 + 2 * h + (lane >> 5);
+            T[q * DP + 2 * (lane & 31)] = v[h].x;
+            T[q * DP + 2 * (lane & 31) + 1] = v[h].y;
+        }
     }
-    if (tid == 0) sfail = 0;
-    __syncthreads();
+    for (int q = 0; q < 64; ++q) X[q * DP + lane] = 0.0;
+    STAMP();
+    const int r = lane & 15;
     for (int kb = 0; kb < 4; ++kb) {
         const int o = kb * 16;
-        if (w == 0) {
-            const int r = lane & 15;
-            double row[16];
+        // (a) factor the 16x16 diagonal block
+        double row[16], yv[16], dv[16];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) row[c] = T[o + r][o + c];
-            bool bad = false;
-            double rinv[16];
+        for (int c = 0; c < 16; ++c) row[c] = T[(o + r) * DP + o + c];
+        bool bad = false;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const double p = rdlane(row[j], j);
-                bad |= !(p > 0.0);
-                // 1/sqrt(p) by v_rsq_f64 + two Newton steps; d = p / sqrt(p)
-                double yv = __builtin_amdgcn_rsq(p);
-                yv = yv * (1.5 - 0.5 * p * yv * yv);
-                yv = yv * (1.5 - 0.5 * p * yv * yv);
-                const double d = p * yv;
-                rinv[j] = yv;
-                row[j] = (r > j) ? row[j] * yv : ((r == j) ? d : row[j]);
+        for (int j = 0; j < 16; ++j) {
+            const double p = rdlane(row[j], j);
+            bad |= !(p > 0.0);
+            double y = __builtin_amdgcn_rsq(p);
+            y = y * (1.5 - 0.5 * p * y * y);
+            y = y * (1.5 - 0.5 * p * y * y);
+            yv[j] = y;
+            dv[j] = p * y;
+            row[j] = (r > j) ? row[j] * y : ((r == j) ? dv[j] : row[j]);
+            if (lane < 16) colb[r] = row[j];
 #pragma unroll
-                for (int c = j + 1; c < 16; ++c) row[c] -= row[j] * rdlane(row[j], c);
-            }
-            if (lane < 16) {
+            for (int c = j + 1; c < 16; ++c) row[c] -= row[j] * colb[c];
+        }
+        if (bad) {  // wave-uniform
+            if (lane == 0) live.status[b] = fail_code;
+            return;
+        }
+        if (lane < 16) {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) T[o + r][o + c] = (c <= r) ? row[c] : 0.0;
-            }
-            // lane c (< 16): column c of inv(L_bb) by forward substitution
-            const int c = lane & 15;
+            for (int c = 0; c < 16; ++c) T[(o + r) * DP + o + c] = (c <= r) ? row[c] : 0.0;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) dg[o + j] = dv[j];
+        }
+        // inverse of the 16x16 factor: lane c (< 16) solves for column c
+        {
+            const int c = r;
             double x[16];
 #pragma unroll
             for (int rr = 0; rr < 16; ++rr) {
-                double s = (rr == c) ? 1.0 : 0.0;
+                double sacc = (rr == c) ? 1.0 : 0.0;
 #pragma unroll
-                for (int m = 0; m < rr; ++m) s -= rdlane(row[m], rr) * x[m];
-                x[rr] = (rr >= c) ? s * rinv[rr] : 0.0;
+                for (int m = 0; m < rr; ++m) sacc -= T[(o + rr) * DP + o + m] * x[m];
+                x[rr] = (rr >= c) ? sacc * yv[rr] : 0.0;
             }
             if (lane < 16) {
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) Xi[o + rr][o + c] = x[rr];
+                for (int rr = 0; rr < 16; ++rr) X[(o + rr) * DP + o + c] = x[rr];
             }
-            if (lane < 16) sdg[o + lane] = row[lane];  // lane r: L[r][r] sits in row[r]
-            if (lane == 0 && bad) sfail = 1;
-        }
-        __syncthreads();
-        STAMP();
-        if (sfail) {
-            if (tid == 0) live.status[b] = fail_code;
-            return;
         }
         if (kb == 3) break;
-        // panel: T[i][c] = sum_{m=o}^{c} T[i][m] * inv[c][m],  i in [o+16, 64), c in [o, o+16)
-        const int nel = (48 - o) * 16;
-        double pv[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int e = tid + q * 256;
-            pv[q] = 0.0;
-            if (e < nel) {
-                const int i = o + 16 + (e >> 4), c = o + (e & 15);
-                double s = 0.0;
-                for (int m = o; m <= c; ++m) s += T[i][m] * Xi[c][m];
-                pv[q] = s;
+        // (b) panel: T[ib][kb] = T[ib][kb] * inv(L_kb,kb)^T for the blocks below
+        for (int ib = kb + 1; ib < 4; ++ib) {
+            d4_t acc = {0.0, 0.0, 0.0, 0.0};
+            mm16_nt<false>(acc, &T[(16 * ib) * DP + o], DP, &X[o * DP + o], DP, lane);
+            st16(acc, &T[(16 * ib) * DP + o], DP, lane, 1.0);
+        }
+        // (c) rank-16 trailing update of the lower blocks
+        for (int ib = kb + 1; ib < 4; ++ib)
+            for (int jb = kb + 1; jb <= ib; ++jb) {
+                d4_t acc;
+                ld16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane);
+                mm16_nt<true>(acc, &T[(16 * ib) * DP + o], DP, &T[(16 * jb) * DP + o], DP, lane);
+                st16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane, 1.0);
             }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int e = tid + q * 256;
-            if (e < nel) T[o + 16 + (e >> 4)][o + (e & 15)] = pv[q];
-        }
-        __syncthreads();
-        // rank-16 trailing update of the lower part of T[o+16:, o+16:]
-        const int m0 = o + 16, sz = 64 - m0;
-        for (int e = tid; e < sz * sz; e += 256) {
-            const int i = m0 + e / sz, j = m0 + e % sz;
-            if (j <= i) {
-                double s = T[i][j];
-#pragma unroll
-                for (int m = 0; m < 16; ++m) s -= T[i][o + m] * T[j][o + m];
-                T[i][j] = s;
-            }
-        }
-        __syncthreads();
         STAMP();
     }
     // off-diagonal blocks of the inverse, block row by block row
-    for (int a = 1; a < 4; ++a) {
-        // Tmp[b'] = sum_{kk=b'}^{a-1} L_{a,kk} X_{kk,b'}   for b' < a
-        for (int e = tid; e < a * 256; e += 256) {
-            const int bb = e >> 8, r = (e >> 4) & 15, c = e & 15;
-            double s = 0.0;
-            for (int m = bb * 16; m < a * 16; ++m) s += T[a * 16 + r][m] * Xi[m][bb * 16 + c];
-            Tmp[bb][r][c] = s;
+    for (int a = 1; a < 4; ++a)
+        for (int bb = 0; bb < a; ++bb) {
+            d4_t acc = {0.0, 0.0, 0.0, 0.0};
+            for (int kk = bb; kk < a; ++kk)
+                mm16_nn(acc, &T[(16 * a) * DP + 16 * kk], DP, &X[(16 * kk) * DP + 16 * bb], DP,
+                        lane);
+            st16(acc, Tmp, 17, lane, 1.0);
+            d4_t acc2 = {0.0, 0.0, 0.0, 0.0};
+            mm16_nn(acc2, &X[(16 * a) * DP + 16 * a], DP, Tmp, 17, lane);
+            st16(acc2, &X[(16 * a) * DP + 16 * bb], DP, lane, -1.0);
         }
-        __syncthreads();
-        // X_{a,b'} = -X_aa Tmp[b']
-        for (int e = tid; e < a * 256; e += 256) {
-            const int bb = e >> 8, r = (e >> 4) & 15, c = e & 15;
-            double s = 0.0;
-            for (int m = 0; m <= r; ++m) s -= Xi[a * 16 + r][a * 16 + m] * Tmp[bb][m][c];
-            Xi[a * 16 + r][bb * 16 + c] = s;
-        }
-        __syncthreads();
-    }
     STAMP();
     double* D = Dinv + b * dstride + (int64_t)k * 4096;
-    for (int e = tid; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        At[(int64_t)r * A.ld + c] = (c <= r) ? T[r][c] : 0.0;
-        D[e] = Xi[r][c];
+    for (int q = 0; q < 64; ++q) {
+        At[(int64_t)q * A.ld + lane] = (lane <= q) ? T[q * DP + lane] : 0.0;
+        D[q * 64 + lane] = X[q * DP + lane];
     }
-    if (w == 0) {  // sum of log L_ii, one lane per pivot
-        const double l = wave_sum_d(log(sdg[lane]));
-        if (lane == 0) ldet[b * lstride + k] = l;
-    }
+    const double l = wave_sum_d(log(dg[lane]));
+    if (lane == 0) ldet[b * lstride + k] = l;
 #ifdef APM_DIAG_STAMPS
     STAMP();
-    if (tid == 0 && k == 0 && b == 0)
+    if (lane == 0 && k == 0 && b == 0)
         for (int q = 0; q < ns; ++q) g_diag_stamps[q] = stamps[q] - stamps[0];
 #endif
 }
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
                       Live live, int fail_code, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_chol_diag, dim3(nchains), dim3(256), 0, s, A, k, Dinv, dstride, ldet,
+    hipLaunchKernelGGL(k_chol_diag, dim3(nchains), dim3(64), 0, s, A, k, Dinv, dstride, ldet,
                        lstride, live, fail_code);
 }
 
@@ -347,28 +363,8 @@ void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t
 
 // ------------------------------------------------------------------------------- trailing update
 // A_ij -= sum_{q<kc} A_{i,k0+q} A_{j,k0+q}^T for tiles i in [i0, R), j in [j0, min(i, jend-1)]
-// (i0 >= j0). Enumerated as a triangular part (rows i < jend: i-j0+1 tiles) followed by a
-// rectangular part (rows i >= jend: jend-j0 tiles).
-__device__ __forceinline__ void decode_update_tile(long t, int i0, int R, int j0, int jend, int& i,
-                                                   int& j) {
-    const int a0 = i0 - j0 + 1;
-    const int ntri_rows = max(0, min(R, jend) - i0);
-    const long ntri = (long)ntri_rows * a0 + (long)ntri_rows * (ntri_rows - 1) / 2;
-    if (t < ntri) {
-        const double aa = a0 - 0.5;
-        long p = (long)floor(-aa + sqrt(aa * aa + 2.0 * (double)t));
-        while (p > 0 && p * a0 + p * (p - 1) / 2 > t) --p;
-        while ((p + 1) * a0 + (p + 1) * p / 2 <= t) ++p;
-        i = i0 + (int)p;
-        j = j0 + (int)(t - (p * a0 + p * (p - 1) / 2));
-    } else {
-        const long r = t - ntri;
-        const int wdt = jend - j0;
-        i = max(i0, jend) + (int)(r / wdt);
-        j = j0 + (int)(r % wdt);
-    }
-}
-
+// (i0 >= j0): a triangular part (rows i < jend: i-j0+1 tiles) and a rectangular part (rows
+// i >= jend: jend-j0 tiles).
 long update_tile_count(int i0, int R, int j0, int jend) {
     if (jend <= j0 || R <= i0) return 0;
     const long a0 = i0 - j0 + 1;
@@ -379,13 +375,27 @@ long update_tile_count(int i0, int R, int j0, int jend) {
     return n;
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc, int i0, int R,
-                                                     int j0, int jend, Live live) {
-    const int b = blockIdx.y;
+// Work item w -> (chain, tile) with an XCD-aware remap: workgroups are dealt round-robin over the
+// 8 XCDs (MI355X_MICROARCH.md, dispatch), so XCD x = L % 8 is given the contiguous work range
+// [x*q+min(x,r), ...) (bijective for any count). Consecutive work items are consecutive tiles of
+// one chain in the host-built super-tile order (8x8 tiles: 8 row panels + 8 column panels = 2 MiB
+// of operands per super-tile), so the operand panels a workgroup needs are in its XCD's L2.
+__device__ __forceinline__ long xcd_remap(long L, long total) {
+    const long xcd = L & 7, q = total >> 3, r = total & 7;
+    const long base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (L >> 3);
+}
+
+__global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc,
+                                                     const unsigned* __restrict__ tiles, int ntiles,
+                                                     int nchains, Live live) {
+    const long total = (long)ntiles * nchains;
+    const long w = xcd_remap(blockIdx.x, total);
+    const int b = (int)(w / ntiles);
     if (!chain_live(live, b)) return;
-    int i, j;
-    decode_update_tile(blockIdx.x, i0, R, j0, jend, i, j);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+    const unsigned ij = tiles[w % ntiles];
+    const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     double* Ab = A.base + b * A.cstride;
     double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
     __shared__ GemmSmem sm;
@@ -396,13 +406,25 @@ __global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc, int
     tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
 }
 
-void launch_chol_update(MatB A, int k0, int kc, int i0, int R, int j0, int jend, Live live,
+void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                         int nchains, hipStream_t s) {
-    if (i0 < j0) i0 = j0;
-    const long n = update_tile_count(i0, R, j0, jend);
-    if (n <= 0) return;
-    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)n, nchains), dim3(256), 0, s, A, k0, kc, i0,
-                       R, j0, jend, live);
+    if (ntiles <= 0) return;
+    const long total = (long)ntiles * nchains;
+    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
+                       ntiles, nchains, live);
+}
+
+// Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
+// super-rows top-down, super-columns left-right, row-major inside), packed (i << 16) | j.
+std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend) {
+    std::vector<unsigned> v;
+    const int S = 8;
+    for (int I = i0; I < R; I += S)
+        for (int J = j0; J < jend; J += S)
+            for (int i = I; i < std::min(I + S, R); ++i)
+                for (int j = J; j < std::min(J + S, jend); ++j)
+                    if (j <= i) v.push_back(((unsigned)i << 16) | (unsigned)j);
+    return v;
 }
 
 // ------------------------------------------------------------------------------- L^T z = r
