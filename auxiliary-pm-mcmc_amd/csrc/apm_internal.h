@@ -33,6 +33,10 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend);
+// 128x128-per-workgroup variant for the rank-256 outer updates (list of 2x2 tile groups)
+void launch_chol_update_big(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int R,
+                            int jend, Live live, int nchains, hipStream_t s);
+std::vector<unsigned> build_update_tiles_big(int i0, int R, int j0, int jend);
 // one step (block J) of the backward solve L^T z = r, r stored in row `rrow` of A (in place),
 // z written to z[b*zstride + ...]
 void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,

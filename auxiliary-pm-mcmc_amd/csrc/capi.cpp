@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -52,13 +53,14 @@ struct apm_ctx {
     SlotSet Sl{};
     UPool Up{};
     std::vector<void*> allocs;
+    bool big_update = false;  // APM_BIG_UPDATE=1 selects the 128x128 kernel for outer updates
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<ProfRec> recs;
     // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
-    std::map<std::tuple<int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
+    std::map<std::tuple<int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
 };
 
 namespace {
@@ -134,7 +136,7 @@ Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
 // rank-256 update per outer panel (4x less read-modify-write traffic than rank-64 steps).
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
-static const int OUTER = 4;
+static int OUTER = 4;  // tiles per outer panel (APM_OUTER overrides, development knob)
 
 double update_flops(int i0, int R, int j0, int jend, int kc) {
     double f = 0.0;
@@ -146,11 +148,12 @@ double update_flops(int i0, int R, int j0, int jend, int kc) {
     return f;
 }
 
-std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend) {
-    auto key = std::make_tuple(i0, R, j0, jend);
+std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend, bool big) {
+    auto key = std::make_tuple(i0, R, j0, jend, (int)big);
     auto it = c->tile_lists.find(key);
     if (it != c->tile_lists.end()) return it->second;
-    std::vector<unsigned> v = build_update_tiles(i0, R, j0, jend);
+    std::vector<unsigned> v =
+        big ? build_update_tiles_big(i0, R, j0, jend) : build_update_tiles(i0, R, j0, jend);
     unsigned* d = dalloc<unsigned>(c, v.size());
     HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
     auto val = std::make_pair(d, (int)v.size());
@@ -161,10 +164,16 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend)
 void tracked_update(apm_ctx* c, int k0, int kc, int i0, int R, int j0, int jend, int count) {
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
-    const auto tl = tile_list(c, i0, R, j0, jend);
+    // wide updates (outer, rank 256) use the 128x128 kernel; narrow inner ones the 64x64 kernel
+    const bool big = c->big_update && kc > 1 && (jend - j0) >= 4;
+    const auto tl = tile_list(c, i0, R, j0, jend, big);
     ProfScope ps(c, APM_PROF_CHOL_UPDATE,
                  c->prof ? update_flops(i0, R, j0, jend, kc) * count : 0.0);
-    launch_chol_update(c->A, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
+    if (big)
+        launch_chol_update_big(c->A, k0, kc, tl.first, tl.second, R, jend, live_of(c), count,
+                               c->stream);
+    else
+        launch_chol_update(c->A, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
     check_launch();
 }
 
@@ -330,6 +339,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t ldx, const double* y, double eps, int64_t S, int64_t max_batch,
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
+    if (const char* e = getenv("APM_BIG_UPDATE")) c->big_update = atoi(e) != 0;
+    if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
     HIPC(hipSetDevice(device));
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->kind = kind;

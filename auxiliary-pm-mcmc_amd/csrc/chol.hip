@@ -80,13 +80,16 @@ __device__ __forceinline__ void tile_acc_store(const d4_t (&acc)[2][2], double* 
                   (lane & 15)] = acc[bi][bj][r];
 }
 
-// acc += (NEG ? -1 : 1) * A[64 x 16*nsub] * B[64 x 16*nsub]^T for the workgroup's 64x64 tile.
-// Operands are staged through LDS in 16-deep slices shared by the four waves (half the L2
-// traffic of per-wave loads), double-buffered: the global loads of slice s+1 are in flight
-// while the MFMAs of slice s run; one barrier per slice. LDS pitch 17 doubles makes the
-// fragment reads (16 rows x 2 k per 32-lane group) bank-conflict free for ds_read_b64.
-#define KSUB 16
-#define LPITCH 17
+// acc += (NEG ? -1 : 1) * A[64 x depth] * B[64 x depth]^T for the workgroup's 64x64 tile.
+// Operands are staged through LDS in KS-deep slices shared by the four waves (half the L2 traffic
+// of per-wave loads), double-buffered: the global loads of slice s+1 are in flight while the
+// MFMAs of slice s run; one barrier per slice. LDS pitch KS+1 doubles keeps the fragment reads
+// (16 rows x 2 k per 32-lane group) bank-conflict free for ds_read_b64.
+#ifndef UPD_KS
+#define UPD_KS 16
+#endif
+#define KSUB UPD_KS
+#define LPITCH (UPD_KS + 1)
 struct GemmSmem {
     double a[2][64][LPITCH];
     double b[2][64][LPITCH];
@@ -95,30 +98,37 @@ struct GemmSmem {
 template <bool NEG>
 __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __restrict__ A,
                                              int64_t lda, const double* __restrict__ B,
-                                             int64_t ldb, int nsub, GemmSmem& sm) {
+                                             int64_t ldb, int depth, GemmSmem& sm) {
+    constexpr int PPR = KSUB / 2;          // 16-byte pieces per row of a slice
+    constexpr int PPT = 64 * PPR / 256;    // pieces per thread per operand
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
     const int r16 = lane & 15, kq = lane >> 4;
-    // staging map: 512 pieces of 16 B per operand slice (64 rows x 128 B); thread -> pieces
-    // tid and tid+256: row = p >> 3, col = (p & 7) * 2
-    const int pr0 = tid >> 3, pc = (tid & 7) * 2, pr1 = pr0 + 32;
-    d2_t ra0, ra1, rb0, rb1;
+    int prow[PPT], pcol[PPT];
+#pragma unroll
+    for (int h = 0; h < PPT; ++h) {
+        const int p = tid + 256 * h;
+        prow[h] = p / PPR;
+        pcol[h] = (p % PPR) * 2;
+    }
+    d2_t ra[PPT], rb[PPT];
     auto gload = [&](int sidx) {
-        const int kc = sidx * KSUB + pc;
-        ra0 = *reinterpret_cast<const d2_t*>(A + (int64_t)pr0 * lda + kc);
-        ra1 = *reinterpret_cast<const d2_t*>(A + (int64_t)pr1 * lda + kc);
-        rb0 = *reinterpret_cast<const d2_t*>(B + (int64_t)pr0 * ldb + kc);
-        rb1 = *reinterpret_cast<const d2_t*>(B + (int64_t)pr1 * ldb + kc);
+#pragma unroll
+        for (int h = 0; h < PPT; ++h) {
+            const int kc = sidx * KSUB + pcol[h];
+            ra[h] = *reinterpret_cast<const d2_t*>(A + (int64_t)prow[h] * lda + kc);
+            rb[h] = *reinterpret_cast<const d2_t*>(B + (int64_t)prow[h] * ldb + kc);
+        }
     };
     auto sstore = [&](int buf) {
-        sm.a[buf][pr0][pc] = NEG ? -ra0.x : ra0.x;
-        sm.a[buf][pr0][pc + 1] = NEG ? -ra0.y : ra0.y;
-        sm.a[buf][pr1][pc] = NEG ? -ra1.x : ra1.x;
-        sm.a[buf][pr1][pc + 1] = NEG ? -ra1.y : ra1.y;
-        sm.b[buf][pr0][pc] = rb0.x;
-        sm.b[buf][pr0][pc + 1] = rb0.y;
-        sm.b[buf][pr1][pc] = rb1.x;
-        sm.b[buf][pr1][pc + 1] = rb1.y;
+#pragma unroll
+        for (int h = 0; h < PPT; ++h) {
+            sm.a[buf][prow[h]][pcol[h]] = NEG ? -ra[h].x : ra[h].x;
+            sm.a[buf][prow[h]][pcol[h] + 1] = NEG ? -ra[h].y : ra[h].y;
+            sm.b[buf][prow[h]][pcol[h]] = rb[h].x;
+            sm.b[buf][prow[h]][pcol[h] + 1] = rb[h].y;
+        }
     };
+    const int nsub = depth / KSUB;
     gload(0);
     sstore(0);
     __syncthreads();
@@ -126,7 +136,7 @@ __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __
         const int cur = s & 1;
         if (s + 1 < nsub) gload(s + 1);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < KSUB / 4; ++t) {
             double a[2], b[2];
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi) a[bi] = sm.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(MatB A, int k, int i0, const
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
-    tile_gemm_nt<false>(acc, At, A.ld, D, 64, 4, sm);  // X = A_ik * inv(L_kk)^T
+    tile_gemm_nt<false>(acc, At, A.ld, D, 64, 64, sm);  // X = A_ik * inv(L_kk)^T
     tile_acc_store(acc, At, A.ld, wr, wc, lane);  // A_ik fully staged before the last barrier
 }
 
@@ -402,7 +412,7 @@ __global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc,
     d4_t acc[2][2];
     tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
     tile_gemm_nt<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
-                       Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 4 * kc, sm);
+                       Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm);
     tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
 }
 
@@ -412,6 +422,140 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
                        ntiles, nchains, live);
+}
+
+// ------------------------------------------------------------------------------- 128x128 update
+// Outer (rank-256) updates: one workgroup per 2x2 group of 64-tiles; wave (wr, wc) owns sub-tile
+// (i+wr, j+wc) as 4x4 v_mfma_f64_16x16x4 accumulators (128 VGPRs), so each 16-deep LDS slice
+// feeds 64 MFMAs per wave from 8 fragment reads (twice the operand reuse of the 64x64 kernel).
+// Sub-tiles outside the update region (above the diagonal, past R or jend) skip their MFMAs and
+// stores; out-of-range operand rows are clamped to a valid row and their results discarded.
+struct BigSmem {
+    double a[2][128][17];
+    double b[2][128][17];
+};
+
+__global__ __launch_bounds__(256) void k_chol_update_big(MatB A, int k0, int kc,
+                                                         const unsigned* __restrict__ tiles,
+                                                         int ntiles, int nchains, int R, int jend,
+                                                         Live live) {
+    const long total = (long)ntiles * nchains;
+    const long w = xcd_remap(blockIdx.x, total);
+    const int b = (int)(w / ntiles);
+    if (!chain_live(live, b)) return;
+    const unsigned ij = tiles[w % ntiles];
+    const int i0 = (int)(ij >> 16), j0 = (int)(ij & 0xffff);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int ti = i0 + wr, tj = j0 + wc;
+    const bool valid = ti < R && tj < jend && tj <= ti;
+    double* Ab = A.base + b * A.cstride;
+    __shared__ BigSmem sm;
+    d4_t acc[4][4];
+    double* Aij = Ab + (int64_t)(ti * 64) * A.ld + tj * 64;
+    if (valid) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[bi][bj][q] = Aij[(int64_t)(16 * bi + F64_CROW(lane, q)) * A.ld + 16 * bj + r16];
+    }
+    // staging: 1024 pieces of 16 B per operand slice (128 rows x 128 B); thread -> 4 pieces
+    const int pc = (tid & 7) * 2;
+    const double* pa[4];
+    const double* pb[4];
+    int prow[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int row = (tid >> 3) + 32 * h;  // 0..127
+        prow[h] = row;
+        const int ra = min(i0 * 64 + row, R * 64 - 1);
+        const int rb = min(j0 * 64 + row, R * 64 - 1);
+        pa[h] = Ab + (int64_t)ra * A.ld + k0 * 64 + pc;
+        pb[h] = Ab + (int64_t)rb * A.ld + k0 * 64 + pc;
+    }
+    d2_t ra_[4], rb_[4];
+    const int nsub = 4 * kc;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        ra_[h] = *reinterpret_cast<const d2_t*>(pa[h]);
+        rb_[h] = *reinterpret_cast<const d2_t*>(pb[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        sm.a[0][prow[h]][pc] = -ra_[h].x;
+        sm.a[0][prow[h]][pc + 1] = -ra_[h].y;
+        sm.b[0][prow[h]][pc] = rb_[h].x;
+        sm.b[0][prow[h]][pc + 1] = rb_[h].y;
+    }
+    __syncthreads();
+    for (int sl = 0; sl < nsub; ++sl) {
+        const int cur = sl & 1;
+        if (sl + 1 < nsub) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                ra_[h] = *reinterpret_cast<const d2_t*>(pa[h] + (sl + 1) * 16);
+                rb_[h] = *reinterpret_cast<const d2_t*>(pb[h] + (sl + 1) * 16);
+            }
+        }
+        if (valid) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                double av[4], bv[4];
+#pragma unroll
+                for (int bi = 0; bi < 4; ++bi) av[bi] = sm.a[cur][64 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+                for (int bj = 0; bj < 4; ++bj) bv[bj] = sm.b[cur][64 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+                for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 4; ++bj)
+                        acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], bv[bj],
+                                                                            acc[bi][bj], 0, 0, 0);
+            }
+        }
+        if (sl + 1 < nsub) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                sm.a[cur ^ 1][prow[h]][pc] = -ra_[h].x;
+                sm.a[cur ^ 1][prow[h]][pc + 1] = -ra_[h].y;
+                sm.b[cur ^ 1][prow[h]][pc] = rb_[h].x;
+                sm.b[cur ^ 1][prow[h]][pc + 1] = rb_[h].y;
+            }
+        }
+        __syncthreads();
+    }
+    if (valid) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    Aij[(int64_t)(16 * bi + F64_CROW(lane, q)) * A.ld + 16 * bj + r16] = acc[bi][bj][q];
+    }
+}
+
+void launch_chol_update_big(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int R,
+                            int jend, Live live, int nchains, hipStream_t s) {
+    if (ntiles <= 0) return;
+    const long total = (long)ntiles * nchains;
+    hipLaunchKernelGGL(k_chol_update_big, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
+                       ntiles, nchains, R, jend, live);
+}
+
+// Host: 2x2 groups (top-left tile (i, j)) covering the update region, in super-tile order
+std::vector<unsigned> build_update_tiles_big(int i0, int R, int j0, int jend) {
+    std::vector<unsigned> v;
+    const int S = 8;
+    for (int I = i0; I < R; I += S)
+        for (int J = j0; J < jend; J += S)
+            for (int i = I; i < std::min(I + S, R); i += 2)
+                for (int j = J; j < std::min(J + S, jend); j += 2)
+                    if (j <= i + 1) v.push_back(((unsigned)i << 16) | (unsigned)j);
+    return v;
 }
 
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
@@ -479,7 +623,7 @@ __global__ __launch_bounds__(256) void k_tile_nt_test(const double* A, const dou
     __shared__ GemmSmem sm;
     d4_t acc[2][2];
     tile_acc_load(acc, C, 64, wr, wc, lane);
-    tile_gemm_nt<false>(acc, A, 64, B, 64, 4, sm);
+    tile_gemm_nt<false>(acc, A, 64, B, 64, 64, sm);
     tile_acc_store(acc, C, 64, wr, wc, lane);
 }
 
