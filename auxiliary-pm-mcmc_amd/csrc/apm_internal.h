@@ -25,14 +25,16 @@ struct Live {
 //         A_ij -= sum_{q<kc} A_{i,k0+q} A_{j,k0+q}^T  (f64 MFMA, rank 64*kc)
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
                       Live live, int fail_code, int nchains, hipStream_t s);
-void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
-                       Live live, int nchains, hipStream_t s);
+// panel rows [i0, R) minus the row tiles [glo, ghi) (pass glo = ghi = R for none)
+void launch_chol_panel(MatB A, int k, int i0, int R, int glo, int ghi, const double* Dinv,
+                       int64_t dstride, Live live, int nchains, hipStream_t s);
 // tiles: device list of packed (i << 16) | j built by build_update_tiles (super-tile order)
-void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                        int nchains, hipStream_t s);
+// plus = true adds instead of subtracting (SYRK of the UL factorisation, postcov.hip)
+void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+                        Live live, int nchains, hipStream_t s);
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
-std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend);
+std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo = 0, int ghi = 0);
 // 128x128-per-workgroup variant for the rank-256 outer updates (list of 2x2 tile groups)
 void launch_chol_update_big(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int R,
                             int jend, Live live, int nchains, hipStream_t s);
@@ -88,11 +90,24 @@ struct SlotSet {
     double* cst;        // 1 per slot: -1/2|g|^2 - 1/2 log|B|  (0 for PriorMC)
     int64_t lstride, vstride;
 };
-// write slot slots[b] from the factored work matrix. mode 0 = IS (C_chol at offset (np,np),
-// g in row 2np), mode 1 = PriorMC (K_chol at (0,0), g = 0)
+// write slot slots[b] from the factored work matrix. mode 0 = IS via the augmented matrix (C_chol
+// at offset (np,np), g in row 2np), mode 1 = PriorMC (K_chol at (0,0), g = 0), mode 2 = IS via
+// chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb)
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s);
+
+// ---- postcov.hip ----------------------------------------------------------------------------
+void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,
+                    Live live, int nchains, hipStream_t s);
+void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Live live,
+                    int nchains, hipStream_t s);
+void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride, int np,
+                    Live live, int nchains, hipStream_t s);
+void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s);
+void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s);
+void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
+                        int nchains, hipStream_t s);
 
 // ---- ugemm.hip ------------------------------------------------------------------------------
 struct UPool {

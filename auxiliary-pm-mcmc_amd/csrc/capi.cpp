@@ -53,14 +53,15 @@ struct apm_ctx {
     SlotSet Sl{};
     UPool Up{};
     std::vector<void*> allocs;
-    bool big_update = false;  // APM_BIG_UPDATE=1 selects the 128x128 kernel for outer updates
+    bool big_update = false;
+    bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix  // APM_BIG_UPDATE=1 selects the 128x128 kernel for outer updates
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<ProfRec> recs;
     // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
-    std::map<std::tuple<int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
+    std::map<std::tuple<int, int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
 };
 
 namespace {
@@ -138,9 +139,20 @@ Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
 static int OUTER = 4;  // tiles per outer panel (APM_OUTER overrides, development knob)
 
-double update_flops(int i0, int R, int j0, int jend, int kc) {
+// Row tiles [lo, hi) known to be zero in panel column k (skipped by panel and update).
+struct Gap {
+    int lo, hi;
+};
+typedef Gap (*GapFn)(int k, int nb);
+Gap no_gap(int, int) { return Gap{0, 0}; }
+// [[J M J],[L_K J]] factorisation (postcov.hip): row tile nb+I of L_K J is zero in every column
+// tile k < nb-1-I, so at column k only bottom rows >= 2nb-1-k are nonzero.
+Gap y_gap(int k, int nb) { return Gap{nb, std::max(nb, 2 * nb - 1 - k)}; }
+
+double update_flops(int i0, int R, int j0, int jend, int kc, Gap g) {
     double f = 0.0;
     for (int i = i0; i < R; ++i) {
+        if (i >= g.lo && i < g.hi) continue;
         const int jmax = std::min(i, jend - 1);
         for (int j = j0; j <= jmax; ++j)
             f += (i == j) ? 64.0 * 65.0 * 64.0 * kc : 2.0 * 64.0 * 64.0 * 64.0 * kc;
@@ -148,12 +160,13 @@ double update_flops(int i0, int R, int j0, int jend, int kc) {
     return f;
 }
 
-std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend, bool big) {
-    auto key = std::make_tuple(i0, R, j0, jend, (int)big);
+std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g,
+                                    bool big) {
+    auto key = std::make_tuple(i0, R, j0, jend, (int)big, g.lo, g.hi);
     auto it = c->tile_lists.find(key);
     if (it != c->tile_lists.end()) return it->second;
-    std::vector<unsigned> v =
-        big ? build_update_tiles_big(i0, R, j0, jend) : build_update_tiles(i0, R, j0, jend);
+    std::vector<unsigned> v = big ? build_update_tiles_big(i0, R, j0, jend)
+                                  : build_update_tiles(i0, R, j0, jend, g.lo, g.hi);
     unsigned* d = dalloc<unsigned>(c, v.size());
     HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
     auto val = std::make_pair(d, (int)v.size());
@@ -161,39 +174,44 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
     return val;
 }
 
-void tracked_update(apm_ctx* c, int k0, int kc, int i0, int R, int j0, int jend, int count) {
+void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
+                    bool plus, int count) {
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
-    // wide updates (outer, rank 256) use the 128x128 kernel; narrow inner ones the 64x64 kernel
-    const bool big = c->big_update && kc > 1 && (jend - j0) >= 4;
-    const auto tl = tile_list(c, i0, R, j0, jend, big);
+    // wide updates (outer, rank 256) may use the 128x128 kernel; narrow inner ones the 64x64 one
+    const bool big = c->big_update && !plus && g.hi <= g.lo && kc > 1 && (jend - j0) >= 4;
+    const auto tl = tile_list(c, i0, R, j0, jend, g, big);
+    if (tl.second <= 0) return;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE,
-                 c->prof ? update_flops(i0, R, j0, jend, kc) * count : 0.0);
+                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0);
     if (big)
-        launch_chol_update_big(c->A, k0, kc, tl.first, tl.second, R, jend, live_of(c), count,
+        launch_chol_update_big(M, k0, kc, tl.first, tl.second, R, jend, live_of(c), count,
                                c->stream);
     else
-        launch_chol_update(c->A, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
+        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream);
     check_launch();
 }
 
-void chol_range(apm_ctx* c, int k0, int k1, int R, int Cb, int fail_code, int count,
-                bool factor_diag = true, int row_start = 0) {
+void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
+                bool factor_diag = true, int row_start = 0, GapFn gap = no_gap) {
     const Live lv = live_of(c);
     for (int K = k0; K < k1; K += OUTER) {
         const int Kend = std::min(K + OUTER, k1);
         for (int k = K; k < Kend; ++k) {
             if (factor_diag) {
-                launch_chol_diag(c->A, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv,
-                                 fail_code, count, c->stream);
+                launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
+                                 count, c->stream);
                 check_launch();
             }
-            launch_chol_panel(c->A, k, std::max(k + 1, row_start), R, c->Dinv, c->dstride, lv,
-                              count, c->stream);
+            const Gap g = gap(k, c->nb);
+            launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv,
+                              c->dstride, lv, count, c->stream);
             check_launch();
-            tracked_update(c, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, count);
+            tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false,
+                           count);
         }
-        tracked_update(c, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb, count);
+        tracked_update(c, M, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb,
+                       gap(Kend - 1, c->nb), false, count);
     }
 }
 
@@ -226,7 +244,7 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h) {
         check_launch();
         launch_form_B(c->K, c->A, c->v, c->np, lv, count, c->stream);
         check_launch();
-        chol_range(c, 0, c->nb, c->nb + 1, c->nb, APM_STATUS_CHOL_B, count);
+        chol_range(c, c->A, 0, c->nb, c->nb + 1, c->nb, APM_STATUS_CHOL_B, count);
         for (int J = c->nb - 1; J >= 0; --J) {
             launch_trsv_lt_step(c->A, J, rrow, c->Dinv, c->dstride, c->v.z, c->v.vstride, lv,
                                 count, c->stream);
@@ -269,8 +287,41 @@ void augmented(apm_ctx* c, int count, bool factor_C) {
     check_launch();
     const int nb = c->nb, R = 2 * nb + 1, Cb = 2 * nb;
     // top-left L (and its diagonal-block inverses) are the last Newton factorisation
-    chol_range(c, 0, nb, R, Cb, APM_STATUS_CHOL_B, count, /*factor_diag=*/false, /*rows>=*/nb);
-    if (factor_C) chol_range(c, nb, 2 * nb, R, Cb, APM_STATUS_CHOL_C, count);
+    chol_range(c, c->A, 0, nb, R, Cb, APM_STATUS_CHOL_B, count, /*factor_diag=*/false, /*rows>=*/nb);
+    if (factor_C) chol_range(c, c->A, nb, 2 * nb, R, Cb, APM_STATUS_CHOL_C, count);
+}
+
+// Posterior-covariance factor through chol(K) (postcov.hip): 4N^3/3 flops instead of the
+// augmented 7N^3/3. Leaves chol(C) J in rows [np, 2np) x cols [0, np) of A, g in v.Kb and
+// log|B| = log|M| in ldet[0..nb).
+void post_cov_lk(apm_ctx* c, int count) {
+    const Live lv = live_of(c);
+    hipStream_t s = c->stream;
+    HIPC(hipMemsetD32Async(c->active, 1, count, s));
+    const int nb = c->nb, np = c->np;
+    const int64_t vs = c->v.vstride;
+    MatB TL = c->A;
+    MatB BL{c->A.base + (int64_t)np * c->A.ld, c->A.ld, c->A.cstride};
+    launch_copy_lower(c->K, BL, np, lv, count, s);
+    check_launch();
+    launch_set_rhs(c->A, 2 * (int64_t)np, np, c->v.f, vs, lv, count, s);  // f_post under K
+    check_launch();
+    chol_range(c, BL, 0, nb, nb + 1, nb, APM_STATUS_CHOL_K, count);       // L_K, h = L_K^-1 f
+    launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
+    check_launch();
+    launch_form_y2(BL, TL, np, c->v.Ws, vs, np, lv, count, s);           // Y2 = J Z^T J
+    check_launch();
+    launch_reverse_cols(BL, np, lv, count, s);                           // Y = L_K J
+    check_launch();
+    launch_identity_lower(TL, np, lv, count, s);
+    check_launch();
+    for (int K = 0; K < nb; K += OUTER) {  // J M J = I + Y2 Y2^T (Y2 lower: j >= K suffices)
+        const int Kend = std::min(K + OUTER, nb);
+        tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, true, count);
+    }
+    chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
+    launch_trmv_lt_rev(TL, c->v.z, c->v.Kb, vs, np, lv, count, s);       // g = J L'^T J h
+    check_launch();
 }
 
 void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf, int* status,
@@ -290,7 +341,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     if (est == APM_EST_PRIORMC) {
         launch_copy_lower(c->K, c->A, c->np, lv, count, c->stream);
         check_launch();
-        chol_range(c, 0, c->nb, c->nb, c->nb, APM_STATUS_CHOL_K, count);
+        chol_range(c, c->A, 0, c->nb, c->nb, c->nb, APM_STATUS_CHOL_K, count);
         launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 1, c->n,
                           c->np, lv, count, c->stream);
         check_launch();
@@ -302,9 +353,15 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                                c->stream);
             check_launch();
         } else {
-            augmented(c, count, true);
-            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 0, c->n,
-                              c->np, lv, count, c->stream);
+            int mode = 2;
+            if (c->postcov_aug) {
+                augmented(c, count, true);
+                mode = 0;
+            } else {
+                post_cov_lk(c, count);
+            }
+            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, mode,
+                              c->n, c->np, lv, count, c->stream);
             check_launch();
             u_eval_device(c, count);
         }
@@ -341,6 +398,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->device = device;
     if (const char* e = getenv("APM_BIG_UPDATE")) c->big_update = atoi(e) != 0;
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
+    if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
     HIPC(hipSetDevice(device));
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->kind = kind;

@@ -346,11 +346,13 @@ void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet
 }
 
 // ------------------------------------------------------------------------------- panel TRSM
-__global__ __launch_bounds__(256) void k_chol_panel(MatB A, int k, int i0, const double* Dinv,
-                                                    int64_t dstride, Live live) {
+__global__ __launch_bounds__(256) void k_chol_panel(MatB A, int k, int i0, int glo, int ghi,
+                                                    const double* Dinv, int64_t dstride,
+                                                    Live live) {
     const int b = blockIdx.y;
     if (!chain_live(live, b)) return;
-    const int i = i0 + blockIdx.x;
+    int i = i0 + blockIdx.x;
+    if (i >= glo) i += ghi - glo;  // skip the row tiles [glo, ghi) (known-zero rows)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
     double* At = A.base + b * A.cstride + (int64_t)(i * 64) * A.ld + k * 64;
     const double* D = Dinv + b * dstride + (int64_t)k * 4096;
@@ -364,10 +366,14 @@ __global__ __launch_bounds__(256) void k_chol_panel(MatB A, int k, int i0, const
     tile_acc_store(acc, At, A.ld, wr, wc, lane);  // A_ik fully staged before the last barrier
 }
 
-void launch_chol_panel(MatB A, int k, int i0, int R, const double* Dinv, int64_t dstride,
-                       Live live, int nchains, hipStream_t s) {
-    if (R <= i0) return;
-    hipLaunchKernelGGL(k_chol_panel, dim3(R - i0, nchains), dim3(256), 0, s, A, k, i0, Dinv,
+void launch_chol_panel(MatB A, int k, int i0, int R, int glo, int ghi, const double* Dinv,
+                       int64_t dstride, Live live, int nchains, hipStream_t s) {
+    glo = std::max(glo, i0);
+    ghi = std::min(ghi, R);
+    if (ghi <= glo) glo = ghi = R;
+    const int rows = (R - i0) - (ghi - glo);
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_chol_panel, dim3(rows, nchains), dim3(256), 0, s, A, k, i0, glo, ghi, Dinv,
                        dstride, live);
 }
 
@@ -398,7 +404,7 @@ __device__ __forceinline__ long xcd_remap(long L, long total) {
 
 __global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc,
                                                      const unsigned* __restrict__ tiles, int ntiles,
-                                                     int nchains, Live live) {
+                                                     int nchains, int plus, Live live) {
     const long total = (long)ntiles * nchains;
     const long w = xcd_remap(blockIdx.x, total);
     const int b = (int)(w / ntiles);
@@ -411,17 +417,21 @@ __global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc,
     __shared__ GemmSmem sm;
     d4_t acc[2][2];
     tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
-    tile_gemm_nt<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
-                       Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm);
+    const double* Ai = Ab + (int64_t)(i * 64) * A.ld + k0 * 64;
+    const double* Aj = Ab + (int64_t)(j * 64) * A.ld + k0 * 64;
+    if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
+        tile_gemm_nt<false>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm);
+    else
+        tile_gemm_nt<true>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm);
     tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
 }
 
-void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                        int nchains, hipStream_t s) {
+void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+                        Live live, int nchains, hipStream_t s) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, live);
+                       ntiles, nchains, (int)plus, live);
 }
 
 // ------------------------------------------------------------------------------- 128x128 update
@@ -560,14 +570,16 @@ std::vector<unsigned> build_update_tiles_big(int i0, int R, int j0, int jend) {
 
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
 // super-rows top-down, super-columns left-right, row-major inside), packed (i << 16) | j.
-std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend) {
+std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo, int ghi) {
     std::vector<unsigned> v;
     const int S = 8;
     for (int I = i0; I < R; I += S)
         for (int J = j0; J < jend; J += S)
-            for (int i = I; i < std::min(I + S, R); ++i)
+            for (int i = I; i < std::min(I + S, R); ++i) {
+                if (i >= glo && i < ghi) continue;
                 for (int j = J; j < std::min(J + S, jend); ++j)
                     if (j <= i) v.push_back(((unsigned)i << 16) | (unsigned)j);
+            }
     return v;
 }
 

@@ -253,12 +253,14 @@ void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet
 }
 
 // ------------------------------------------------------------------------------- cache slots
-// mode 0 (IS):      L = C_chol (A rows/cols offset np), row np of L = g^T (A row 2np, cols >= np)
-// mode 1 (PriorMC): L = K_chol (A top-left), row np of L = 0
+// mode 0 (IS, augmented): L = C_chol (A rows/cols offset np), row np = g^T (A row 2np, cols >= np)
+// mode 1 (PriorMC):       L = K_chol (A top-left), row np of L = 0
+// mode 2 (IS, chol(K)):   L = (block at rows np.., cols 0..) J, row np = g^T (vector v.Kb)
 // Rows are written whole (upper part zero) because the u-path GEMM streams full row segments.
 __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
                                                       const int64_t* __restrict__ slots, int mode,
-                                                      int np, Live live) {
+                                                      int np, const double* __restrict__ gvec,
+                                                      int64_t gstride, Live live) {
     const int b = blockIdx.y;
     if (live.status[b] != 0) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -266,12 +268,18 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     const double* Ab = A.base + b * A.cstride;
     float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
     const int64_t off = (mode == 0) ? np : 0;
-    if (r < np) {
+    if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
+        const double* src = Ab + ((int64_t)np + r) * A.ld;
+        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? (float)src[np - 1 - c] : 0.0f;
+    } else if (r < np) {
         const double* src = Ab + (off + r) * A.ld + off;
         for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? (float)src[c] : 0.0f;
     } else if (r == np && mode == 0) {
         const double* src = Ab + (2 * (int64_t)np) * A.ld + np;
         for (int c = lane; c < np; c += 64) L[c] = (float)src[c];
+    } else if (r == np && mode == 2) {
+        const double* g = gvec + b * gstride;
+        for (int c = lane; c < np; c += 64) L[c] = (float)g[c];
     } else {
         for (int c = lane; c < np; c += 64) L[c] = 0.0f;
     }
@@ -288,7 +296,7 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
     const int64_t so = slots[b] * S.vstride;
     double gg = 0.0;
     for (int i = threadIdx.x; i < np; i += 256) {
-        const bool is = (mode == 0) && i < n;
+        const bool is = (mode != 1) && i < n;
         const double f = is ? v.f[b * v.vstride + i] : 0.0;
         const double W = is ? v.W[b * v.vstride + i] : 0.0;
         S.fpost[so + i] = (float)f;
@@ -297,12 +305,15 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
         if (mode == 0) {
             const double g = A.base[b * A.cstride + 2 * np * A.ld + np + i];
             gg += g * g;
+        } else if (mode == 2) {
+            const double g = v.Kb[b * v.vstride + i];
+            gg += g * g;
         }
     }
     gg = block_sum_d(gg, red);
     if (threadIdx.x == 0) {
         double c = 0.0;
-        if (mode == 0) {
+        if (mode != 1) {
             double ld = 0.0;
             for (int k = 0; k < nb; ++k) ld += ldet[b * lstride + k];
             c = -0.5 * gg - ld;
@@ -315,7 +326,7 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s) {
     hipLaunchKernelGGL(k_slot_write_L, dim3((np + 64) / 4, nchains), dim3(256), 0, s, A, S, slots,
-                       mode, np, live);
+                       mode, np, v.Kb, v.vstride, live);
     hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
 }

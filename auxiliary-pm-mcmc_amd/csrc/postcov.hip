@@ -1,0 +1,155 @@
+// Posterior-covariance factor of the IS estimator through chol(K).
+//
+// The reference forms C = K - (W^1/2 K)^T B^-1 (W^1/2 K) (latent_posterior_approximations.py:111-112)
+// and factors it (estimators.py:209): TRSM + SYRK + potrf = 7N^3/3 flops. With K = L_K L_K^T,
+//   C = L_K M^-1 L_K^T,   M = I + L_K^T W L_K   (push-through identity, W of the last iteration),
+// and if M = U U^T with U UPPER triangular (the "UL" Cholesky), then C = (L_K U^-T)(L_K U^-T)^T
+// where L_K U^-T is lower triangular with a positive diagonal: it IS chol(C). With J the index
+// reversal, J M J = Y2 Y2^T + I for the lower-triangular Y2 = J Z^T J (Z = W^1/2 L_K), its ordinary
+// Cholesky L' gives U = J L' J, and factoring [[J M J],[L_K J]] yields (L_K J) L'^-T = chol(C) J.
+// Cost: chol(K) + SYRK of a triangle + chol(M) + triangular TRSM = 4N^3/3. Also
+//   g = C_chol^-1 f_post = U^T L_K^-1 f_post = J L'^T J h,  h = L_K^-1 f_post,  log|B| = log|M|.
+#include "apm_internal.h"
+
+__device__ __forceinline__ bool live_pc(const Live& lv, int b) {
+    return lv.active[b] != 0 && lv.status[b] == 0;
+}
+
+// rows [row0, row0+64) of A over columns [0, ncols): row row0 = vec, the others 0
+__global__ __launch_bounds__(256) void k_set_rhs(MatB A, int64_t row0, int ncols,
+                                                 const double* __restrict__ vec, int64_t vstride,
+                                                 Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    double* Ab = A.base + b * A.cstride;
+    const int c0 = blockIdx.x * 64;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int rr = e >> 6, c = c0 + (e & 63);
+        if (c < ncols) Ab[(row0 + rr) * A.ld + c] = (rr == 0) ? vec[b * vstride + c] : 0.0;
+    }
+}
+
+void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,
+                    Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_rhs, dim3((ncols + 63) / 64, nchains), dim3(256), 0, s, A, row0, ncols,
+                       vec, vstride, live);
+}
+
+// copy one row of A (row `row`, columns [0, n)) of every chain into a vector
+__global__ __launch_bounds__(256) void k_get_row(MatB A, int64_t row, int n, double* out,
+                                                 int64_t ostride, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < n) out[b * ostride + c] = A.base[b * A.cstride + row * A.ld + c];
+}
+
+void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Live live,
+                    int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_get_row, dim3((n + 255) / 256, nchains), dim3(256), 0, s, A, row, n, out,
+                       ostride, live);
+}
+
+// Y2[a][k'] = W^1/2[np-1-k'] * L[np-1-k'][np-1-a] for k' <= a, 0 above (all np x np of dst from
+// column dcol0), where L is the lower factor held in `src`. Lower tile (ta, tk') of dst is the
+// reversed transpose of the source tile (nb-1-tk', nb-1-ta), staged through LDS.
+__global__ __launch_bounds__(256) void k_form_y2(MatB src, MatB dst, int64_t dcol0,
+                                                 const double* __restrict__ Ws, int64_t vstride,
+                                                 int nb, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int ta = blockIdx.x / nb, tk = blockIdx.x % nb;
+    const int np = nb * 64;
+    double* D = dst.base + b * dst.cstride + (int64_t)(ta * 64) * dst.ld + dcol0 + tk * 64;
+    if (tk > ta) {  // upper tiles are read as zeros by the SYRK's panel-wide k-range
+        for (int e = threadIdx.x; e < 4096; e += 256) D[(int64_t)(e >> 6) * dst.ld + (e & 63)] = 0.0;
+        return;
+    }
+    const int sr = nb - 1 - tk, sc = nb - 1 - ta;  // source tile (lower: sr >= sc)
+    __shared__ double T[64][65];
+    const double* S = src.base + b * src.cstride + (int64_t)(sr * 64) * src.ld + sc * 64;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        T[r][c] = (sr > sc || c <= r) ? S[(int64_t)r * src.ld + c] : 0.0;
+    }
+    __syncthreads();
+    const double* w = Ws + b * vstride;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int al = e >> 6, kl = e & 63;  // local output row (a) and column (k')
+        const int kg = tk * 64 + kl;
+        D[(int64_t)al * dst.ld + kl] = w[np - 1 - kg] * T[63 - kl][63 - al];
+    }
+}
+
+void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride, int np,
+                    Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_form_y2, dim3(nb * nb, nchains), dim3(256), 0, s, src, dst,
+                       dcol0, Ws, vstride, nb, live);
+}
+
+// in place: Y = L J restricted to L's lower triangle (the rest of L is treated as zero)
+__global__ __launch_bounds__(256) void k_reverse_cols(MatB M, int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int half = np / 2;
+    if (e >= (int64_t)np * half) return;
+    const int i = (int)(e / half), c = (int)(e % half), c2 = np - 1 - c;
+    double* row = M.base + b * M.cstride + (int64_t)i * M.ld;
+    const double l1 = (c <= i) ? row[c] : 0.0, l2 = (c2 <= i) ? row[c2] : 0.0;
+    row[c] = l2;
+    row[c2] = l1;
+}
+
+void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s) {
+    const int64_t tot = (int64_t)np * (np / 2);
+    hipLaunchKernelGGL(k_reverse_cols, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0,
+                       s, M, np, live);
+}
+
+// lower tiles of M <- I
+__global__ __launch_bounds__(256) void k_identity_lower(MatB M, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    int ti = (int)floor((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > (int)blockIdx.x) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= (int)blockIdx.x) ++ti;
+    const int tj = blockIdx.x - ti * (ti + 1) / 2;
+    double* D = M.base + b * M.cstride + (int64_t)(ti * 64) * M.ld + tj * 64;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        D[(int64_t)r * M.ld + c] = (ti == tj && r == c) ? 1.0 : 0.0;
+    }
+}
+
+void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_identity_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, M, live);
+}
+
+// g = J L'^T J h: g[np-1-c] = sum_{r >= c} L'[r][c] h[np-1-r]; one workgroup per 64-column block,
+// each wave strides over rows (512-byte coalesced row segments), waves reduced through LDS.
+__global__ __launch_bounds__(256) void k_trmv_lt_rev(MatB L, const double* __restrict__ h,
+                                                     double* __restrict__ g, int64_t vstride,
+                                                     int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = cb * 64 + lane;
+    const double* Lb = L.base + b * L.cstride;
+    const double* hb = h + b * vstride;
+    double s = 0.0;
+    for (int r = cb * 64 + w; r < np; r += 4)
+        if (r >= c) s += Lb[(int64_t)r * L.ld + c] * hb[np - 1 - r];
+    __shared__ double red[4][64];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0) g[b * vstride + np - 1 - c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
+                        int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_trmv_lt_rev, dim3(np / 64, nchains), dim3(256), 0, s, L, h, g, vstride, np,
+                       live);
+}

@@ -48,10 +48,10 @@ int main(int argc, char** argv) {
         unsigned* dt;
         hipMalloc(&dt, 4 * t.size());
         hipMemcpy(dt, t.data(), 4 * t.size(), hipMemcpyHostToDevice);
-        for (int w = 0; w < 2; ++w) launch_chol_update(M, c.k0, c.kc, dt, (int)t.size(), lv, chains, 0);
+        for (int w = 0; w < 2; ++w) launch_chol_update(M, c.k0, c.kc, dt, (int)t.size(), false, lv, chains, 0);
         hipEventRecord(e0);
         const int reps = 5;
-        for (int w = 0; w < reps; ++w) launch_chol_update(M, c.k0, c.kc, dt, (int)t.size(), lv, chains, 0);
+        for (int w = 0; w < reps; ++w) launch_chol_update(M, c.k0, c.kc, dt, (int)t.size(), false, lv, chains, 0);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
