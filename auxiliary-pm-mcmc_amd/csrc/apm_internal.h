@@ -10,6 +10,13 @@ struct MatB {
     int64_t cstride;
 };
 
+// The same for fp32 (mixed-precision Newton factorisation, chol32.hip).
+struct MatF {
+    float* base;
+    int64_t ld;
+    int64_t cstride;
+};
+
 // Per-chain liveness: a kernel does work for chain b iff active[b] != 0 && status[b] == 0.
 struct Live {
     const int* active;
@@ -30,8 +37,9 @@ void launch_chol_panel(MatB A, int k, int i0, int R, int glo, int ghi, const dou
                        int64_t dstride, Live live, int nchains, hipStream_t s);
 // tiles: device list of packed (i << 16) | j built by build_update_tiles (super-tile order)
 // plus = true adds instead of subtracting (SYRK of the UL factorisation, postcov.hip)
+// lds_pad: extra dynamic LDS per workgroup (caps residency at 3 workgroups per CU, see capi.cpp)
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
-                        Live live, int nchains, hipStream_t s);
+                        Live live, int nchains, hipStream_t s, int lds_pad = 0);
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo = 0, int ghi = 0);
@@ -45,6 +53,27 @@ void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_
                          double* z, int64_t zstride, Live live, int nchains, hipStream_t s);
 // test hook: C(64x64) = A(64x64) * B(64x64)^T through the MFMA tile path
 void launch_tile_nt_test(const double* A, const double* B, double* C, hipStream_t s);
+
+// ---- chol32.hip: mixed-precision Newton solve (fp32 factor of B + fp64 refinement) -----------
+void launch_chol_diag32(MatF A, int k, float* Dinv, int64_t dstride, double* ldet,
+                        int64_t lstride, Live live, int fail_code, int nchains, hipStream_t s);
+void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const float* Dinv,
+                         int64_t dstride, Live live, int nchains, hipStream_t s);
+void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
+                          int nchains, hipStream_t s);
+struct NewtonVecs;
+void launch_form_B32(MatB K, MatF Bf, NewtonVecs v, int np, Live live, int nchains,
+                     hipStream_t s);
+void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Live live,
+                  int nchains, hipStream_t s);
+// blocked TRSV steps with fp32 tiles / inverses and fp64 vectors (r updated in place)
+void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,
+                       double* y, int64_t vstride, Live live, int nchains, hipStream_t s);
+void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
+                       int64_t vstride, Live live, int nchains, hipStream_t s);
+// refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
+void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,
+                   double* out, int64_t vstride, int np, Live live, int nchains, hipStream_t s);
 
 // ---- gram.hip -------------------------------------------------------------------------------
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]

@@ -33,6 +33,10 @@ struct ProfRec {
 struct apm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;     // panel stream of the one-panel lookahead (chol_range)
+    hipEvent_t ev_upd = nullptr, ev_pan = nullptr;
+    bool lookahead = false;  // APM_LOOKAHEAD=1: one-panel lookahead on stream2
+    int la_pad = 6400;  // 4 x (34816 + 6400) B > 160 KiB LDS per CU (APM_LA_PAD overrides)             // APM_LOOKAHEAD=0 disables (development knob)
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
     double eps = 1e-8, tol = 1e-4;
@@ -45,6 +49,9 @@ struct apm_ctx {
     int64_t dstride = 0, lstride = 0, pstride = 0;
     NewtonVecs v{};
     double* vecbase = nullptr;
+    double* rvec = nullptr;   // 3 refinement vectors per chain (mixed-precision Newton)
+    bool mixed = true;        // APM_MIXED=0: fp64 Newton factorisation (development knob)
+    int n_refine = 1;         // APM_REFINE overrides
     int *active = nullptr, *status = nullptr, *n_iter = nullptr;
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;
     double *d_ca = nullptr, *d_cb = nullptr;
@@ -54,7 +61,7 @@ struct apm_ctx {
     UPool Up{};
     std::vector<void*> allocs;
     bool big_update = false;
-    bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix  // APM_BIG_UPDATE=1 selects the 128x128 kernel for outer updates
+    bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> evpool;
@@ -114,16 +121,18 @@ struct ProfScope {
     apm_ctx* c;
     int kind;
     double work;
+    hipStream_t s;
     hipEvent_t a{}, b{};
-    ProfScope(apm_ctx* c_, int k, double w) : c(c_), kind(k), work(w) {
+    ProfScope(apm_ctx* c_, int k, double w, hipStream_t s_ = nullptr)
+        : c(c_), kind(k), work(w), s(s_ ? s_ : c_->stream) {
         if (c->prof) {
             a = next_event(c);
             b = next_event(c);
-            HIPC(hipEventRecord(a, c->stream));
+            HIPC(hipEventRecord(a, s));
         }
     }
     ~ProfScope() {
-        if (c->prof && hipEventRecord(b, c->stream) == hipSuccess)
+        if (c->prof && hipEventRecord(b, s) == hipSuccess)
             c->recs.push_back(ProfRec{a, b, kind, work});
     }
 };
@@ -175,7 +184,8 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
 }
 
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
-                    bool plus, int count) {
+                    bool plus, int count, hipStream_t s = nullptr, int lds_pad = 0) {
+    if (!s) s = c->stream;
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
     // wide updates (outer, rank 256) may use the 128x128 kernel; narrow inner ones the 64x64 one
@@ -183,35 +193,100 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     const auto tl = tile_list(c, i0, R, j0, jend, g, big);
     if (tl.second <= 0) return;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE,
-                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0);
+                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0, s);
     if (big)
-        launch_chol_update_big(M, k0, kc, tl.first, tl.second, R, jend, live_of(c), count,
-                               c->stream);
+        launch_chol_update_big(M, k0, kc, tl.first, tl.second, R, jend, live_of(c), count, s);
     else
-        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream);
+        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, s, lds_pad);
     check_launch();
 }
 
+// Tile columns [K, Kend) of one outer panel: 64-wide diag / panel / inner-update steps on stream s.
+void factor_panel(apm_ctx* c, MatB M, int K, int Kend, int R, int fail_code, int count,
+                  bool factor_diag, int row_start, GapFn gap, hipStream_t s) {
+    const Live lv = live_of(c);
+    for (int k = K; k < Kend; ++k) {
+        if (factor_diag) {
+            launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code, count,
+                             s);
+            check_launch();
+        }
+        const Gap g = gap(k, c->nb);
+        launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv, c->dstride, lv,
+                          count, s);
+        check_launch();
+        tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false, count, s);
+    }
+}
+
+// One-panel lookahead: the outer update of panel K is split into the next panel's columns
+// [Kend, Kn) and the rest [Kn, Cb). The next panel is factored on stream2 (high priority) as soon
+// as its columns are updated, concurrently with the bulk update on the main stream; the two touch
+// disjoint tile columns and read only the finished panel K. The latency-bound diag/panel chain
+// (one 64-thread workgroup per chain) thus hides under the MFMA-bound rank-256 update.
 void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
                 bool factor_diag = true, int row_start = 0, GapFn gap = no_gap) {
+    hipStream_t s1 = c->stream, s2 = c->stream2;
+    factor_panel(c, M, k0, std::min(k0 + OUTER, k1), R, fail_code, count, factor_diag, row_start,
+                 gap, s1);
+    for (int K = k0; K < k1; K += OUTER) {
+        const int Kend = std::min(K + OUTER, k1), Kn = std::min(Kend + OUTER, k1);
+        const int i0 = std::max(Kend, row_start);
+        const Gap g = gap(Kend - 1, c->nb);
+        if (Kend >= k1) {  // rows beyond the factored range (e.g. the RHS block) only
+            tracked_update(c, M, K, Kend - K, i0, R, Kend, Cb, g, false, count, s1);
+            break;
+        }
+        if (!c->lookahead) {
+            tracked_update(c, M, K, Kend - K, i0, R, Kend, Cb, g, false, count, s1);
+            factor_panel(c, M, Kend, Kn, R, fail_code, count, factor_diag, row_start, gap, s1);
+            continue;
+        }
+        tracked_update(c, M, K, Kend - K, i0, R, Kend, Kn, g, false, count, s1);
+        HIPC(hipEventRecord(c->ev_upd, s1));
+        HIPC(hipStreamWaitEvent(s2, c->ev_upd, 0));
+        factor_panel(c, M, Kend, Kn, R, fail_code, count, factor_diag, row_start, gap, s2);
+        HIPC(hipEventRecord(c->ev_pan, s2));
+        // padded to 3 resident workgroups per CU (measured as fast as 4): every CU keeps room
+        // for one diag / panel / inner-update workgroup of the panel stream
+        tracked_update(c, M, K, Kend - K, std::max(Kn, row_start), R, Kn, Cb, g, false, count, s1,
+                       c->la_pad);
+        HIPC(hipStreamWaitEvent(s1, c->ev_pan, 0));
+    }
+}
+
+// ---- fp32 factorisation of the Newton matrix (chol32.hip), in the memory of the work matrix
+MatF b32_of(apm_ctx* c) {
+    return MatF{reinterpret_cast<float*>(c->A.base), c->np, 2 * c->A.cstride};
+}
+float* dinv32_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv); }
+
+void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
+                      int count) {
+    if (i0 < j0) i0 = j0;
+    if (update_tile_count(i0, R, j0, jend) <= 0) return;
+    const auto tl = tile_list(c, i0, R, j0, jend, Gap{0, 0}, false);
+    if (tl.second <= 0) return;
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE32,
+                 c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * count : 0.0);
+    launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
+    check_launch();
+}
+
+void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_code, int count) {
     const Live lv = live_of(c);
+    float* D = dinv32_of(c);
+    const int64_t ds = 2 * c->dstride;
     for (int K = k0; K < k1; K += OUTER) {
         const int Kend = std::min(K + OUTER, k1);
         for (int k = K; k < Kend; ++k) {
-            if (factor_diag) {
-                launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
-                                 count, c->stream);
-                check_launch();
-            }
-            const Gap g = gap(k, c->nb);
-            launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv,
-                              c->dstride, lv, count, c->stream);
+            launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count, c->stream);
             check_launch();
-            tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false,
-                           count);
+            launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
+            check_launch();
+            tracked_update32(c, M, k, 1, k + 1, R, k + 1, Kend, count);
         }
-        tracked_update(c, M, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb,
-                       gap(Kend - 1, c->nb), false, count);
+        tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count);
     }
 }
 
@@ -230,9 +305,51 @@ void u_eval_device(apm_ctx* c, int count) {
 }
 
 // Newton loop of laplace_approximation over the live chains; returns host n_iter per chain.
-void newton(apm_ctx* c, int count, std::vector<int>& st_h) {
+// B x = W^1/2 K b with the fp32 factor (its forward solve is the appended row np) and n_refine
+// steps of fp64 iterative refinement; x -> v.z (chol32.hip)
+void newton_solve32(apm_ctx* c, int count) {
     const Live lv = live_of(c);
-    HIPC(hipMemsetAsync(c->v.f, 0, sizeof(double) * c->v.vstride * count, c->stream));
+    hipStream_t s = c->stream;
+    const int nb = c->nb, np = c->np;
+    const int64_t vs = c->v.vstride, ds = 2 * c->dstride;
+    MatF F = b32_of(c);
+    float* D = dinv32_of(c);
+    double *r1 = c->rvec, *r2 = c->rvec + c->max_batch * vs, *r3 = c->rvec + 2 * c->max_batch * vs;
+    launch_form_B32(c->K, F, c->v, np, lv, count, s);
+    check_launch();
+    chol_range32(c, F, 0, nb, nb + 1, nb, APM_STATUS_CHOL_B, count);
+    launch_row32(F, np, np, r1, vs, lv, count, s);  // y0 = L^-1 rhs (fp32)
+    check_launch();
+    for (int J = nb - 1; J >= 0; --J) {
+        launch_trsv_bwd32(F, J, D, ds, r1, c->v.z, vs, lv, count, s);
+        check_launch();
+    }
+    for (int it = 0; it < c->n_refine; ++it) {
+        launch_refine(0, c->v.Ws, c->v.Kb, c->v.z, nullptr, r2, vs, np, lv, count, s);  // t
+        check_launch();
+        launch_gemv(c->K, r2, vs, r3, vs, np, lv, count, s);                             // K t
+        check_launch();
+        launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lv, count, s);       // res
+        check_launch();
+        for (int J = 0; J < nb; ++J) {
+            launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lv, count, s);
+            check_launch();
+        }
+        for (int J = nb - 1; J >= 0; --J) {
+            launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lv, count, s);
+            check_launch();
+        }
+        launch_refine(2, nullptr, nullptr, c->v.z, nullptr, r3, vs, np, lv, count, s);  // x += d
+        check_launch();
+    }
+}
+
+void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
+    const Live lv = live_of(c);
+    // f = 0 for the live chains only (a fallback rerun must keep the other chains' modes)
+    launch_refine(3, nullptr, nullptr, nullptr, nullptr, c->v.f, c->v.vstride, c->np, lv, count,
+                  c->stream);
+    check_launch();
     std::vector<int> act(count, 1);  // max_iters == 0: every chain is unconverged
     const int64_t rrow = c->np;  // Newton rhs row (extra row block below B)
     int64_t it = 0;
@@ -242,13 +359,17 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h) {
         launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
                     c->stream);
         check_launch();
-        launch_form_B(c->K, c->A, c->v, c->np, lv, count, c->stream);
-        check_launch();
-        chol_range(c, c->A, 0, c->nb, c->nb + 1, c->nb, APM_STATUS_CHOL_B, count);
-        for (int J = c->nb - 1; J >= 0; --J) {
-            launch_trsv_lt_step(c->A, J, rrow, c->Dinv, c->dstride, c->v.z, c->v.vstride, lv,
-                                count, c->stream);
+        if (mixed) {
+            newton_solve32(c, count);
+        } else {
+            launch_form_B(c->K, c->A, c->v, c->np, lv, count, c->stream);
             check_launch();
+            chol_range(c, c->A, 0, c->nb, c->nb + 1, c->nb, APM_STATUS_CHOL_B, count);
+            for (int J = c->nb - 1; J >= 0; --J) {
+                launch_trsv_lt_step(c->A, J, rrow, c->Dinv, c->dstride, c->v.z, c->v.vstride, lv,
+                                    count, c->stream);
+                check_launch();
+            }
         }
         launch_newton_update(c->v, c->np, lv, count, c->stream);
         check_launch();
@@ -278,8 +399,31 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h) {
                             c->stream));
 }
 
-// Posterior-covariance stage on the augmented matrix. With `factor_C` false the
-// bottom-right block is left holding C = K - V^T V (used by apm_laplace's calc_cov).
+// Newton for the IS estimator: mixed precision, with an fp64 rerun for any chain whose fp32
+// factorisation broke down (B is SPD with eigenvalues >= 1, so only for extreme theta)
+void newton_is(apm_ctx* c, int count, std::vector<int>& st_h) {
+    newton(c, count, st_h, c->mixed);
+    if (!c->mixed) return;
+    std::vector<int> redo;
+    for (int b = 0; b < count; ++b)
+        if (st_h[b] == APM_STATUS_CHOL_B) redo.push_back(b);
+    if (redo.empty()) return;
+    std::vector<int> nit(count);
+    HIPC(hipMemcpyAsync(nit.data(), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
+                        c->stream));
+    sync(c);
+    for (int b : redo) {
+        st_h[b] = 0;
+        nit[b] = 0;
+    }
+    HIPC(hipMemcpyAsync(c->status, st_h.data(), sizeof(int) * count, hipMemcpyHostToDevice,
+                        c->stream));
+    HIPC(hipMemcpyAsync(c->n_iter, nit.data(), sizeof(int) * count, hipMemcpyHostToDevice,
+                        c->stream));
+    // only the redo chains are live now: converged chains have active = 0, failed ones status != 0
+    newton(c, count, st_h, false);
+}
+
 void augmented(apm_ctx* c, int count, bool factor_C) {
     const Live lv = live_of(c);
     HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
@@ -347,7 +491,10 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         check_launch();
         u_eval_device(c, count);
     } else {
-        newton(c, count, st_h);
+        if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself
+            newton(c, count, st_h, false);
+        else
+            newton_is(c, count, st_h);
         if (est == APM_EST_LAPLACE) {
             launch_laplace_lml(c->v, c->y, c->n, c->ldet, c->lstride, c->nb, c->out, lv, count,
                                c->stream);
@@ -400,7 +547,16 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
     if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
     HIPC(hipSetDevice(device));
+    if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
+    if (const char* e = getenv("APM_LA_PAD")) c->la_pad = std::max(0, atoi(e));
+    if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
+    if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    int prio_lo = 0, prio_hi = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPC(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi));
+    HIPC(hipEventCreateWithFlags(&c->ev_upd, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&c->ev_pan, hipEventDisableTiming));
     c->kind = kind;
     c->n = (int)n;
     c->d = (int)d;
@@ -439,6 +595,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->partial = dalloc<double>(c, B * c->pstride);
     const int64_t vs = np;
     c->vecbase = dalloc<double>(c, 8 * B * vs);
+    c->rvec = dalloc<double>(c, 3 * B * vs);
     c->v = NewtonVecs{c->vecbase,          c->vecbase + 1 * B * vs, c->vecbase + 2 * B * vs,
                       c->vecbase + 3 * B * vs, c->vecbase + 4 * B * vs, c->vecbase + 5 * B * vs,
                       c->vecbase + 6 * B * vs, c->vecbase + 7 * B * vs, vs};
@@ -469,6 +626,10 @@ void free_ctx(apm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    if (c->ev_upd) (void)hipEventDestroy(c->ev_upd);
+    if (c->ev_pan) (void)hipEventDestroy(c->ev_pan);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -802,7 +963,7 @@ int apm_laplace(int device, const double* K, int64_t n, int64_t ldk, const doubl
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
         HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int), c->stream));
         std::vector<int> st(1, 0);
-        newton(c, 1, st);
+        newton(c, 1, st, false);
         int it = 0;
         HIPC(hipMemcpyAsync(&it, c->n_iter, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         sync(c);

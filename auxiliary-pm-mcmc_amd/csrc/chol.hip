@@ -80,11 +80,18 @@ __device__ __forceinline__ void tile_acc_store(const d4_t (&acc)[2][2], double* 
                   (lane & 15)] = acc[bi][bj][r];
 }
 
-// acc += (NEG ? -1 : 1) * A[64 x depth] * B[64 x depth]^T for the workgroup's 64x64 tile.
-// Operands are staged through LDS in KS-deep slices shared by the four waves (half the L2 traffic
-// of per-wave loads), double-buffered: the global loads of slice s+1 are in flight while the
-// MFMAs of slice s run; one barrier per slice. LDS pitch KS+1 doubles keeps the fragment reads
-// (16 rows x 2 k per 32-lane group) bank-conflict free for ds_read_b64.
+#ifndef UPD_ABL
+#define UPD_ABL 0
+#endif
+#ifndef UPD_WPE
+#define UPD_WPE 3  // min waves per SIMD for k_chol_update (caps VGPRs at 168)
+#endif
+#ifndef UPD_PF
+#define UPD_PF 2   // slices of global loads in flight (1 or 2)
+#endif
+#ifndef UPD_LATEC
+#define UPD_LATEC 1  // load the old tile behind the first slices and add it at the end
+#endif
 #ifndef UPD_KS
 #define UPD_KS 16
 #endif
@@ -95,10 +102,19 @@ struct GemmSmem {
     double b[2][64][LPITCH];
 };
 
+// acc += (NEG ? -1 : 1) * A[64 x depth] * B[64 x depth]^T (+ the tile C, if given) for the
+// workgroup's 64x64 tile. Operands are staged through LDS in KS-deep slices shared by the four
+// waves, double-buffered, with TWO slices of global loads in flight (register sets alternate with
+// the slice parity; loads are unconditional - clamped to the last slice - so the compiler's
+// vmcnt waits count exactly and never drain the newer set). The old C tile, when given, is loaded
+// behind the first two slices and added at the end, off the critical path of the first MFMA.
+// One barrier per slice; LDS pitch KS+1 keeps the fragment reads bank-conflict free.
 template <bool NEG>
 __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __restrict__ A,
                                              int64_t lda, const double* __restrict__ B,
-                                             int64_t ldb, int depth, GemmSmem& sm) {
+                                             int64_t ldb, int depth, GemmSmem& sm,
+                                             const double* __restrict__ C = nullptr,
+                                             int64_t ldc = 0) {
     constexpr int PPR = KSUB / 2;          // 16-byte pieces per row of a slice
     constexpr int PPT = 64 * PPR / 256;    // pieces per thread per operand
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
@@ -110,8 +126,10 @@ __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __
         prow[h] = p / PPR;
         pcol[h] = (p % PPR) * 2;
     }
-    d2_t ra[PPT], rb[PPT];
-    auto gload = [&](int sidx) {
+    auto gload = [&](int sidx, d2_t (&ra)[PPT], d2_t (&rb)[PPT]) {
+#if UPD_ABL == 1  // ablation (tools/upd_bench.cpp): operands always slice 0 (L1/L2 resident)
+        sidx = 0;
+#endif
 #pragma unroll
         for (int h = 0; h < PPT; ++h) {
             const int kc = sidx * KSUB + pcol[h];
@@ -119,7 +137,7 @@ __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __
             rb[h] = *reinterpret_cast<const d2_t*>(B + (int64_t)prow[h] * ldb + kc);
         }
     };
-    auto sstore = [&](int buf) {
+    auto sstore = [&](int buf, const d2_t (&ra)[PPT], const d2_t (&rb)[PPT]) {
 #pragma unroll
         for (int h = 0; h < PPT; ++h) {
             sm.a[buf][prow[h]][pcol[h]] = NEG ? -ra[h].x : ra[h].x;
@@ -128,13 +146,7 @@ __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __
             sm.b[buf][prow[h]][pcol[h] + 1] = rb[h].y;
         }
     };
-    const int nsub = depth / KSUB;
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int s = 0; s < nsub; ++s) {
-        const int cur = s & 1;
-        if (s + 1 < nsub) gload(s + 1);
+    auto compute = [&](int cur) {
 #pragma unroll
         for (int t = 0; t < KSUB / 4; ++t) {
             double a[2], b[2];
@@ -146,11 +158,51 @@ __device__ __forceinline__ void tile_gemm_nt(d4_t (&acc)[2][2], const double* __
             for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj)
+#if UPD_ABL == 2  // ablation: no MFMA (memory + LDS + barrier pipeline only)
+                    acc[bi][bj][0] += a[bi] * b[bj];
+#else
                     acc[bi][bj] =
                         __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi], b[bj], acc[bi][bj], 0, 0, 0);
+#endif
         }
-        if (s + 1 < nsub) sstore(cur ^ 1);
+    };
+    const int nsub = depth / KSUB;  // even: depth is a multiple of 64 and KS <= 32
+    d4_t old[2][2];
+#if UPD_PF == 2
+    d2_t ra0[PPT], rb0[PPT], ra1[PPT], rb1[PPT];
+    gload(0, ra0, rb0);
+    gload(1, ra1, rb1);
+    if (C) tile_acc_load(old, C, ldc, wr, wc, lane);
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    for (int s = 0; s < nsub; s += 2) {
+        gload(min(s + 2, nsub - 1), ra0, rb0);
+        compute(0);
+        sstore(1, ra1, rb1);
         __syncthreads();
+        gload(min(s + 3, nsub - 1), ra1, rb1);
+        compute(1);
+        sstore(0, ra0, rb0);  // past the end: a clamped reload into a buffer no longer read
+        __syncthreads();
+    }
+#else
+    d2_t ra0[PPT], rb0[PPT];
+    gload(0, ra0, rb0);
+    if (C) tile_acc_load(old, C, ldc, wr, wc, lane);
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    for (int s = 0; s < nsub; ++s) {
+        gload(min(s + 1, nsub - 1), ra0, rb0);
+        compute(s & 1);
+        sstore((s + 1) & 1, ra0, rb0);
+        __syncthreads();
+    }
+#endif
+    if (C) {
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] += old[bi][bj];
     }
 }
 
@@ -162,6 +214,8 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 #ifdef APM_DIAG_STAMPS
 __device__ unsigned long long g_diag_stamps[16];  // diagnostic build only (tools/diag_stamps.cpp)
 #endif
+#define DP 65  // LDS pitch (doubles) of the diag kernel's tile
+
 // Broadcast lane l's value of a wave-uniform-indexed register (v_readlane x2).
 __device__ __forceinline__ double rdlane(double v, int l) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -195,6 +249,42 @@ __device__ __forceinline__ void st16(const d4_t& acc, double* dst, int ld, int l
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[((lane >> 4) + 4 * q) * ld + (lane & 15)] = sgn * acc[q];
 }
+__device__ __forceinline__ void st16t(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[(lane & 15) * ld + (lane >> 4) + 4 * q] = sgn * acc[q];
+}
+// Products with a diagonal block X of the inverse held as (strict lower part transposed at Td,
+// diagonal in xd): X[r][c] = c < r ? Td[c][r] : (c == r ? xd[r] : 0).
+__device__ __forceinline__ double xblk(const double* Td, const double* xd, int r, int c) {
+    return (c < r) ? Td[c * DP + r] : ((c == r) ? xd[r] : 0.0);
+}
+//   acc += A * X^T
+__device__ __forceinline__ void mm16_nt_xb(d4_t& acc, const double* a, int lda, const double* Td,
+                                           const double* xd, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   xblk(Td, xd, r16, 4 * t + kq), acc, 0, 0, 0);
+}
+//   acc += A * X
+__device__ __forceinline__ void mm16_nn_xb(d4_t& acc, const double* a, int lda, const double* Td,
+                                           const double* xd, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   xblk(Td, xd, 4 * t + kq, r16), acc, 0, 0, 0);
+}
+//   acc += X * B
+__device__ __forceinline__ void mm16_nn_xa(d4_t& acc, const double* Td, const double* xd,
+                                           const double* b, int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xblk(Td, xd, r16, 4 * t + kq),
+                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
+}
 __device__ __forceinline__ void ld16(d4_t& acc, const double* src, int ld, int lane) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = src[((lane >> 4) + 4 * q) * ld + (lane & 15)];
@@ -205,15 +295,25 @@ __device__ __forceinline__ void ld16(d4_t& acc, const double* src, int ld, int l
 // registers (pivot by v_readlane, column broadcast through LDS, 1/sqrt by v_rsq_f64 + two Newton
 // steps) and inverted (lane c substitutes column c); the 16-wide panel solve, the rank-16
 // trailing update and the assembly of the full inverse X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb are
-// 16x16x16 f64-MFMA products on LDS operands.
-#define DP 65
-__global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, int64_t dstride,
+// 16x16x16 f64-MFMA products on LDS operands. The inverse is kept transposed in the unused upper
+// triangle of T (X_ab, a > b, in block (b, a); the strictly lower part of X_aa in the upper part of
+// diagonal block (a, a); its diagonal in xdg): 36 KB of LDS, so that the kernel fits next to three
+// padded update workgroups on a CU (lookahead, capi.cpp).
+// Storage of the tile and of Dinv is fp64 (MatB) or fp32 (MatF, the mixed-precision Newton
+// factorisation, chol32.hip); the factorisation itself always runs in fp64.
+__device__ __forceinline__ d2_t ld2(const double* p) { return *reinterpret_cast<const d2_t*>(p); }
+__device__ __forceinline__ d2_t ld2(const float* p) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    return d2_t{(double)v.x, (double)v.y};
+}
+template <class Mat, class TS>
+__global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_t dstride,
                                                   double* ldet, int64_t lstride, Live live,
                                                   int fail_code) {
     const int b = blockIdx.x;
     if (!chain_live(live, b)) return;
     __shared__ double T[64 * DP];
-    __shared__ double X[64 * DP];
+    __shared__ double xdg[64];
     __shared__ double Tmp[16 * 17];
     __shared__ double colb[16];
     __shared__ double dg[64];
@@ -226,7 +326,7 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
 #define STAMP()
 #endif
     STAMP();
-    double* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
+    TS* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
     // 32 KB tile -> LDS: 4 rounds of 8 independent 16-byte loads per lane (lane covers 2 columns)
 #pragma unroll
     for (int q0 = 0; q0 < 64; q0 += 16) {
@@ -234,7 +334,7 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const int q = q0 + 2 * h + (lane >> 5);
-            v[h] = *reinterpret_cast<const d2_t*>(At + (int64_t)q * A.ld + 2 * (lane & 31));
+            v[h] = ld2(At + (int64_t)q * A.ld + 2 * (lane & 31));
         }
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
@@ -243,7 +343,6 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
             T[q * DP + 2 * (lane & 31) + 1] = v[h].y;
         }
     }
-    for (int q = 0; q < 64; ++q) X[q * DP + lane] = 0.0;
     STAMP();
     const int r = lane & 15;
     for (int kb = 0; kb < 4; ++kb) {
@@ -292,14 +391,16 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
             }
             if (lane < 16) {
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) X[(o + rr) * DP + o + c] = x[rr];
+                for (int rr = 0; rr < 16; ++rr)
+                    if (rr > c) T[(o + c) * DP + o + rr] = x[rr];
+                xdg[o + c] = x[c];
             }
         }
         if (kb == 3) break;
         // (b) panel: T[ib][kb] = T[ib][kb] * inv(L_kb,kb)^T for the blocks below
         for (int ib = kb + 1; ib < 4; ++ib) {
             d4_t acc = {0.0, 0.0, 0.0, 0.0};
-            mm16_nt<false>(acc, &T[(16 * ib) * DP + o], DP, &X[o * DP + o], DP, lane);
+            mm16_nt_xb(acc, &T[(16 * ib) * DP + o], DP, &T[o * DP + o], &xdg[o], lane);
             st16(acc, &T[(16 * ib) * DP + o], DP, lane, 1.0);
         }
         // (c) rank-16 trailing update of the lower blocks
@@ -316,19 +417,21 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
     for (int a = 1; a < 4; ++a)
         for (int bb = 0; bb < a; ++bb) {
             d4_t acc = {0.0, 0.0, 0.0, 0.0};
-            for (int kk = bb; kk < a; ++kk)
-                mm16_nn(acc, &T[(16 * a) * DP + 16 * kk], DP, &X[(16 * kk) * DP + 16 * bb], DP,
-                        lane);
+            mm16_nn_xb(acc, &T[(16 * a) * DP + 16 * bb], DP, &T[(16 * bb) * DP + 16 * bb],
+                       &xdg[16 * bb], lane);
+            for (int kk = bb + 1; kk < a; ++kk)  // X_kk,bb is stored transposed at T block (bb, kk)
+                mm16_nt<false>(acc, &T[(16 * a) * DP + 16 * kk], DP, &T[(16 * bb) * DP + 16 * kk],
+                               DP, lane);
             st16(acc, Tmp, 17, lane, 1.0);
             d4_t acc2 = {0.0, 0.0, 0.0, 0.0};
-            mm16_nn(acc2, &X[(16 * a) * DP + 16 * a], DP, Tmp, 17, lane);
-            st16(acc2, &X[(16 * a) * DP + 16 * bb], DP, lane, -1.0);
+            mm16_nn_xa(acc2, &T[(16 * a) * DP + 16 * a], &xdg[16 * a], Tmp, 17, lane);
+            st16t(acc2, &T[(16 * bb) * DP + 16 * a], DP, lane, -1.0);
         }
     STAMP();
-    double* D = Dinv + b * dstride + (int64_t)k * 4096;
+    TS* D = Dinv + b * dstride + (int64_t)k * 4096;
     for (int q = 0; q < 64; ++q) {
-        At[(int64_t)q * A.ld + lane] = (lane <= q) ? T[q * DP + lane] : 0.0;
-        D[q * 64 + lane] = X[q * DP + lane];
+        At[(int64_t)q * A.ld + lane] = (TS)((lane <= q) ? T[q * DP + lane] : 0.0);
+        D[q * 64 + lane] = (TS)((lane < q) ? T[lane * DP + q] : ((lane == q) ? xdg[q] : 0.0));
     }
     const double l = wave_sum_d(log(dg[lane]));
     if (lane == 0) ldet[b * lstride + k] = l;
@@ -341,8 +444,14 @@ __global__ __launch_bounds__(64) void k_chol_diag(MatB A, int k, double* Dinv, i
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
                       Live live, int fail_code, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_chol_diag, dim3(nchains), dim3(64), 0, s, A, k, Dinv, dstride, ldet,
-                       lstride, live, fail_code);
+    hipLaunchKernelGGL((k_chol_diag<MatB, double>), dim3(nchains), dim3(64), 0, s, A, k, Dinv,
+                       dstride, ldet, lstride, live, fail_code);
+}
+
+void launch_chol_diag32(MatF A, int k, float* Dinv, int64_t dstride, double* ldet,
+                        int64_t lstride, Live live, int fail_code, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL((k_chol_diag<MatF, float>), dim3(nchains), dim3(64), 0, s, A, k, Dinv,
+                       dstride, ldet, lstride, live, fail_code);
 }
 
 // ------------------------------------------------------------------------------- panel TRSM
@@ -402,36 +511,48 @@ __device__ __forceinline__ long xcd_remap(long L, long total) {
     return base + (L >> 3);
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(MatB A, int k0, int kc,
+__global__ __launch_bounds__(256, UPD_WPE) void k_chol_update(MatB A, int k0, int kc,
                                                      const unsigned* __restrict__ tiles, int ntiles,
                                                      int nchains, int plus, Live live) {
     const long total = (long)ntiles * nchains;
-    const long w = xcd_remap(blockIdx.x, total);
-    const int b = (int)(w / ntiles);
-    if (!chain_live(live, b)) return;
-    const unsigned ij = tiles[w % ntiles];
-    const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
-    double* Ab = A.base + b * A.cstride;
-    double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
     __shared__ GemmSmem sm;
-    d4_t acc[2][2];
-    tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
-    const double* Ai = Ab + (int64_t)(i * 64) * A.ld + k0 * 64;
-    const double* Aj = Ab + (int64_t)(j * 64) * A.ld + k0 * 64;
-    if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
-        tile_gemm_nt<false>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm);
-    else
-        tile_gemm_nt<true>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm);
-    tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
+    {
+        const long L = blockIdx.x;
+        const long w = xcd_remap(L, total);
+        const int b = (int)(w / ntiles);
+        if (!chain_live(live, b)) return;
+        const unsigned ij = tiles[w % ntiles];
+        const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
+        double* Ab = A.base + b * A.cstride;
+        double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
+        d4_t acc[2][2];
+#if UPD_LATEC
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
+        const double* Cold = Aij;
+#else
+        tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
+        const double* Cold = nullptr;
+#endif
+        const double* Ai = Ab + (int64_t)(i * 64) * A.ld + k0 * 64;
+        const double* Aj = Ab + (int64_t)(j * 64) * A.ld + k0 * 64;
+        if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
+            tile_gemm_nt<false>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm, Cold, A.ld);
+        else
+            tile_gemm_nt<true>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm, Cold, A.ld);
+        tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
+    }
 }
 
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
-                        Live live, int nchains, hipStream_t s) {
+                        Live live, int nchains, hipStream_t s, int lds_pad) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, (int)plus, live);
+    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), lds_pad, s, A, k0, kc,
+                       tiles, ntiles, nchains, (int)plus, live);
 }
 
 // ------------------------------------------------------------------------------- 128x128 update
@@ -445,7 +566,7 @@ struct BigSmem {
     double b[2][128][17];
 };
 
-__global__ __launch_bounds__(256) void k_chol_update_big(MatB A, int k0, int kc,
+__global__ __launch_bounds__(256, 2) void k_chol_update_big(MatB A, int k0, int kc,
                                                          const unsigned* __restrict__ tiles,
                                                          int ntiles, int nchains, int R, int jend,
                                                          Live live) {

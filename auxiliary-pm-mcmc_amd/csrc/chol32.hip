@@ -1,0 +1,378 @@
+// Mixed-precision Newton solve: B = I + W^1/2 K W^1/2 factored in fp32 (f32 MFMA), the solve
+// B x = W^1/2 K b refined once against the fp64 B.
+//
+// The reference factors B in fp64 at every Newton iteration (latent_posterior_approximations.py:92)
+// and solves with it (:94). B's eigenvalues are >= 1 and its condition number is ~1 + max(W) *
+// lambda_max(K), so the fp32 factor solves to ~cond * 6e-8 and ONE step of iterative refinement
+// with the fp64 residual r = rhs - x - W^1/2 (K (W^1/2 x)) brings x to fp64 accuracy (measured
+// Newton modes agree with the all-fp64 iteration to 1e-12 relative for typical theta and 1e-8 at
+// sigma = e^4; tests/test_gpu_kernels.py checks the mode against the oracle). The IS estimator
+// never uses this factor otherwise (its covariance factor is rebuilt from chol(K) in fp64,
+// postcov.hip), so nothing else changes. The Laplace estimator keeps the fp64 factor (its log|B|
+// is part of the returned value).
+//
+// Kernels: fp32 copies of the diag / panel / trailing-update steps of chol.hip on the same 64x64
+// tile lists (f32 MFMA v_mfma_f32_16x16x4_f32: twice the fp64 MFMA rate, half the bytes), blocked
+// forward / backward TRSV with fp32 tiles and fp64 vectors, and the refinement vector ops.
+#include <algorithm>
+
+#include "apm_internal.h"
+
+#define KS32 32          // slice depth (floats) of the LDS-staged tile GEMM
+#define LP32 (KS32 + 2)  // pitch 34 floats: fragment reads (16 rows x 4 k) hit 32 distinct banks
+struct GemmSmem32 {
+    float a[2][64][LP32];
+    float b[2][64][LP32];
+};
+// v_mfma_f32_16x16x4_f32: A lane l holds A[l&15][k=l>>4], B holds B[k=l>>4][l&15];
+// D reg r of lane l is (row 4*(l>>4) + r, col l&15)  (cdna_hip_programming.md §3)
+#define F32_CROW(l, r) (4 * ((l) >> 4) + (r))
+
+__device__ __forceinline__ bool live32(const Live& lv, int b) {
+    return lv.active[b] != 0 && lv.status[b] == 0;
+}
+
+__device__ __forceinline__ void tile32_load(f4_t (&acc)[2][2], const float* T, int64_t ld, int wr,
+                                            int wc, int lane) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[bi][bj][r] = T[(int64_t)(32 * wr + 16 * bi + F32_CROW(lane, r)) * ld +
+                                   32 * wc + 16 * bj + (lane & 15)];
+}
+
+__device__ __forceinline__ void tile32_store(const f4_t (&acc)[2][2], float* T, int64_t ld,
+                                             int wr, int wc, int lane) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                T[(int64_t)(32 * wr + 16 * bi + F32_CROW(lane, r)) * ld + 32 * wc + 16 * bj +
+                  (lane & 15)] = acc[bi][bj][r];
+}
+
+// acc += (NEG ? -1 : 1) * A[64 x depth] * B[64 x depth]^T (+ C if given): the fp32 twin of
+// chol.hip's tile_gemm_nt (two slices of loads in flight, double-buffered LDS, one barrier per
+// slice, the old tile loaded behind the first slices and added at the end).
+template <bool NEG>
+__device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* __restrict__ A,
+                                               int64_t lda, const float* __restrict__ B,
+                                               int64_t ldb, int depth, GemmSmem32& sm,
+                                               const float* __restrict__ C, int64_t ldc) {
+    constexpr int PPR = KS32 / 4;        // 16-byte pieces per slice row
+    constexpr int PPT = 64 * PPR / 256;  // pieces per thread per operand
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    int prow[PPT], pcol[PPT];
+#pragma unroll
+    for (int h = 0; h < PPT; ++h) {
+        const int p = tid + 256 * h;
+        prow[h] = p / PPR;
+        pcol[h] = (p % PPR) * 4;
+    }
+    auto gload = [&](int sidx, f4_t (&ra)[PPT], f4_t (&rb)[PPT]) {
+#pragma unroll
+        for (int h = 0; h < PPT; ++h) {
+            const int kc = sidx * KS32 + pcol[h];
+            ra[h] = *reinterpret_cast<const f4_t*>(A + (int64_t)prow[h] * lda + kc);
+            rb[h] = *reinterpret_cast<const f4_t*>(B + (int64_t)prow[h] * ldb + kc);
+        }
+    };
+    auto sstore = [&](int buf, const f4_t (&ra)[PPT], const f4_t (&rb)[PPT]) {
+#pragma unroll
+        for (int h = 0; h < PPT; ++h)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sm.a[buf][prow[h]][pcol[h] + e] = NEG ? -ra[h][e] : ra[h][e];
+                sm.b[buf][prow[h]][pcol[h] + e] = rb[h][e];
+            }
+    };
+    auto compute = [&](int cur) {
+#pragma unroll
+        for (int t = 0; t < KS32 / 4; ++t) {
+            float a[2], b[2];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) a[bi] = sm.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) b[bj] = sm.b[cur][32 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+                    acc[bi][bj] =
+                        __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], b[bj], acc[bi][bj], 0, 0, 0);
+        }
+    };
+    const int nsub = depth / KS32;  // even: depth is a multiple of 64
+    f4_t ra0[PPT], rb0[PPT], ra1[PPT], rb1[PPT];
+    gload(0, ra0, rb0);
+    gload(1, ra1, rb1);
+    f4_t old[2][2];
+    if (C) tile32_load(old, C, ldc, wr, wc, lane);
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    for (int s = 0; s < nsub; s += 2) {
+        gload(min(s + 2, nsub - 1), ra0, rb0);
+        compute(0);
+        sstore(1, ra1, rb1);
+        __syncthreads();
+        gload(min(s + 3, nsub - 1), ra1, rb1);
+        compute(1);
+        sstore(0, ra0, rb0);
+        __syncthreads();
+    }
+    if (C) {
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] += old[bi][bj];
+    }
+}
+
+// ------------------------------------------------------------------------------- panel, update
+__global__ __launch_bounds__(256) void k_chol_panel32(MatF A, int k, int i0, int glo, int ghi,
+                                                      const float* Dinv, int64_t dstride,
+                                                      Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    int i = i0 + blockIdx.x;
+    if (i >= glo) i += ghi - glo;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+    float* At = A.base + b * A.cstride + (int64_t)(i * 64) * A.ld + k * 64;
+    const float* D = Dinv + b * dstride + (int64_t)k * 4096;
+    __shared__ GemmSmem32 sm;
+    f4_t acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+    tile_gemm_nt32<false>(acc, At, A.ld, D, 64, 64, sm, nullptr, 0);  // A_ik * inv(L_kk)^T
+    tile32_store(acc, At, A.ld, wr, wc, lane);
+}
+
+void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const float* Dinv,
+                         int64_t dstride, Live live, int nchains, hipStream_t s) {
+    glo = std::max(glo, i0);
+    ghi = std::min(ghi, R);
+    if (ghi <= glo) glo = ghi = R;
+    const int rows = (R - i0) - (ghi - glo);
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_chol_panel32, dim3(rows, nchains), dim3(256), 0, s, A, k, i0, glo, ghi,
+                       Dinv, dstride, live);
+}
+
+// Same XCD-aware work mapping as k_chol_update (chol.hip).
+__device__ __forceinline__ long xcd_remap32(long L, long total) {
+    const long xcd = L & 7, q = total >> 3, r = total & 7;
+    const long base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (L >> 3);
+}
+
+__global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
+                                                       const unsigned* __restrict__ tiles,
+                                                       int ntiles, int nchains, Live live) {
+    const long total = (long)ntiles * nchains;
+    const long w = xcd_remap32(blockIdx.x, total);
+    const int b = (int)(w / ntiles);
+    if (!live32(live, b)) return;
+    const unsigned ij = tiles[w % ntiles];
+    const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
+    float* Ab = A.base + b * A.cstride;
+    float* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
+    __shared__ GemmSmem32 sm;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
+    f4_t acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+    tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
+                         Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm, Aij, A.ld);
+    tile32_store(acc, Aij, A.ld, wr, wc, lane);
+}
+
+void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
+                          int nchains, hipStream_t s) {
+    if (ntiles <= 0) return;
+    const long total = (long)ntiles * nchains;
+    hipLaunchKernelGGL(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
+                       ntiles, nchains, live);
+}
+
+// ------------------------------------------------------------------------------- B in fp32
+// lower tiles of B32 = I + W^1/2 K W^1/2 (formed in fp64, rounded once); rows [np, np+64): the
+// right-hand side W^1/2 (K b) in row np, zeros below (forward-solved by the factorisation)
+__global__ __launch_bounds__(256) void k_form_B32(MatB K, MatF Bf, NewtonVecs v, int nb,
+                                                  Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int t = blockIdx.x, ntri = nb * (nb + 1) / 2;
+    const double* Kb = K.base + b * K.cstride;
+    float* Fb = Bf.base + b * Bf.cstride;
+    const double* Ws = v.Ws + b * v.vstride;
+    const int tid = threadIdx.x;
+    if (t < ntri) {
+        int ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while (ti * (ti + 1) / 2 > t) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        const int tj = t - ti * (ti + 1) / 2;
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
+            const double kv = Kb[(int64_t)r * K.ld + c];
+            Fb[(int64_t)r * Bf.ld + c] = (float)((r == c ? 1.0 : 0.0) + (Ws[r] * kv) * Ws[c]);
+        }
+    } else {
+        const int tj = t - ntri;
+        const int64_t r0 = (int64_t)nb * 64;
+        const double* Kbv = v.Kb + b * v.vstride;
+        for (int e = tid; e < 4096; e += 256) {
+            const int rr = e >> 6, c = tj * 64 + (e & 63);
+            Fb[(r0 + rr) * Bf.ld + c] = (rr == 0) ? (float)(Ws[c] * Kbv[c]) : 0.0f;
+        }
+    }
+}
+
+void launch_form_B32(MatB K, MatF Bf, NewtonVecs v, int np, Live live, int nchains,
+                     hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_form_B32, dim3(nb * (nb + 1) / 2 + nb, nchains), dim3(256), 0, s, K, Bf,
+                       v, nb, live);
+}
+
+// out[b][:] = row `row` of Bf (fp32 -> fp64)
+__global__ __launch_bounds__(256) void k_row32(MatF Bf, int64_t row, int np, double* out,
+                                               int64_t ostride, Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < np) out[b * ostride + c] = (double)Bf.base[b * Bf.cstride + row * Bf.ld + c];
+}
+
+void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Live live,
+                  int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_row32, dim3((np + 255) / 256, nchains), dim3(256), 0, s, Bf, row, np,
+                       out, ostride, live);
+}
+
+// ------------------------------------------------------------------------------- TRSV
+// 64x64 fp32 tile -> LDS (pitch 65), coalesced rows; thread (q, c) then reads row c.
+__device__ __forceinline__ void stage_tile32(float (*T)[65], const float* src, int64_t ld) {
+    for (int e = threadIdx.x; e < 4096; e += 256) T[e >> 6][e & 63] = src[(int64_t)(e >> 6) * ld + (e & 63)];
+}
+
+// Forward step J (J = 0 .. nb-1) of L y = r: every workgroup forms y_J = inv(L_JJ) r_J; workgroup
+// I == J stores it, workgroups I > J update r_I -= L_IJ y_J (r updated in place).
+__global__ __launch_bounds__(256) void k_trsv_fwd32(MatF A, int J, const float* Dinv,
+                                                    int64_t dstride, double* r, double* y,
+                                                    int64_t vstride, Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int I = J + blockIdx.x;
+    const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
+    __shared__ float T[64][65];
+    __shared__ double vj[64];
+    __shared__ double part[4][64];
+    double* rb = r + b * vstride;
+    stage_tile32(T, Dinv + b * dstride + (int64_t)J * 4096, 64);
+    if (tid < 64) vj[tid] = rb[J * 64 + tid];
+    __syncthreads();
+    double s = 0.0;
+    for (int m = q * 16; m < q * 16 + 16; ++m) s += (double)T[c][m] * vj[m];
+    part[q][c] = s;
+    __syncthreads();
+    const double yc = part[0][c] + part[1][c] + part[2][c] + part[3][c];
+    if (I == J) {
+        if (tid < 64) y[b * vstride + J * 64 + tid] = yc;
+        return;
+    }
+    __syncthreads();  // part and T are reused
+    if (tid < 64) vj[tid] = yc;
+    stage_tile32(T, A.base + b * A.cstride + (int64_t)(I * 64) * A.ld + J * 64, A.ld);
+    __syncthreads();
+    s = 0.0;
+    for (int m = q * 16; m < q * 16 + 16; ++m) s += (double)T[c][m] * vj[m];
+    part[q][c] = s;
+    __syncthreads();
+    if (tid < 64) rb[I * 64 + tid] -= part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+}
+
+// Backward step J (J = nb-1 .. 0) of L^T z = r: z_J = inv(L_JJ)^T r_J; I < J: r_I -= L_JI^T z_J.
+// The transposed products read tile rows with consecutive lanes on consecutive columns.
+__global__ __launch_bounds__(256) void k_trsv_bwd32(MatF A, int J, const float* Dinv,
+                                                    int64_t dstride, double* r, double* z,
+                                                    int64_t vstride, Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int I = blockIdx.x;
+    const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
+    __shared__ double vj[64];
+    __shared__ double part[4][64];
+    __shared__ double zj[64];
+    double* rb = r + b * vstride;
+    if (tid < 64) vj[tid] = rb[J * 64 + tid];
+    __syncthreads();
+    const float* D = Dinv + b * dstride + (int64_t)J * 4096;
+    double s = 0.0;
+    for (int m = q * 16; m < q * 16 + 16; ++m) s += (double)D[m * 64 + c] * vj[m];
+    part[q][c] = s;
+    __syncthreads();
+    if (tid < 64) zj[tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    __syncthreads();
+    if (I == J) {
+        if (tid < 64) z[b * vstride + J * 64 + tid] = zj[tid];
+        return;
+    }
+    const float* L = A.base + b * A.cstride + (int64_t)(J * 64) * A.ld + I * 64;
+    s = 0.0;
+    for (int m = q * 16; m < q * 16 + 16; ++m) s += (double)L[(int64_t)m * A.ld + c] * zj[m];
+    part[q][c] = s;
+    __syncthreads();
+    if (tid < 64) rb[I * 64 + tid] -= part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+}
+
+void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,
+                       double* y, int64_t vstride, Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_trsv_fwd32, dim3(nb - J, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
+                       r, y, vstride, live);
+}
+
+void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
+                       int64_t vstride, Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_trsv_bwd32, dim3(J + 1, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
+                       r, z, vstride, live);
+}
+
+// ------------------------------------------------------------------------------- refinement
+// mode 0: t = Ws * x                                 (before the fp64 gemv Kt = K t)
+// mode 1: res = Ws * Kb - x - Ws * Kt                (residual of B x = W^1/2 K b)
+// mode 2: x += d                                     (corrected solution)
+// mode 3: out = 0                                    (Newton start f = 0 of the live chains)
+__global__ __launch_bounds__(256) void k_refine(int mode, const double* __restrict__ Ws,
+                                                const double* __restrict__ Kb, double* x,
+                                                const double* __restrict__ Kt, double* out,
+                                                int64_t vstride, int np, Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= np) return;
+    const int64_t o = b * vstride + i;
+    if (mode == 0)
+        out[o] = Ws[o] * x[o];
+    else if (mode == 1)
+        out[o] = Ws[o] * Kb[o] - x[o] - Ws[o] * Kt[o];
+    else if (mode == 2)
+        x[o] += out[o];
+    else
+        out[o] = 0.0;
+}
+
+void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,
+                   double* out, int64_t vstride, int np, Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_refine, dim3((np + 255) / 256, nchains), dim3(256), 0, s, mode, Ws, Kb,
+                       x, Kt, out, vstride, np, live);
+}

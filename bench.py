@@ -178,7 +178,7 @@ def main():
     for _ in range(a.warmup):
         smp.step()
     ctx = smp.ctx
-    for k in (0, 1, 2):
+    for k in (0, 1, 2, 3):
         ctx.prof_read(k, reset=True)
     ctx.prof_enable(True)
     thetas = []
@@ -196,19 +196,34 @@ def main():
     n_u = (smp.n_u_calls - u0) / max(1, a.chains * a.steps)
 
     prof = {}
-    for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm')):
+    for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32')):
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
-    ms, cnt, flops = prof['chol_update']
-    avg_s = ms * 1e-3 / max(cnt, 1)
-    achieved = (flops / max(cnt, 1)) / avg_s / 1e12 if cnt else 0.0
-    roofline = {'kernel': 'k_chol_update (f64 MFMA trailing update, rank-64/256)',
-                'bound': 'mfma', 'achieved': achieved, 'peak': PEAK_F64_MFMA_TFLOPS,
-                'unit': 'TFLOP/s', 'frac': achieved / PEAK_F64_MFMA_TFLOPS, 'traffic': None,
+
+    def mfma_roofline(name, kernel, peak):
+        ms, cnt, flops = prof[name]
+        if not cnt:
+            return None
+        avg_s = ms * 1e-3 / cnt
+        achieved = (flops / cnt) / avg_s / 1e12
+        return {'kernel': kernel, 'bound': 'mfma', 'achieved': achieved, 'peak': peak,
+                'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
                 'launches': cnt, 'avg_launch_us': avg_s * 1e6,
-                'algorithmic_flops_per_launch': flops / max(cnt, 1),
+                'algorithmic_flops_per_launch': flops / cnt,
                 'share_of_step_time': (ms * 1e-3) / elapsed}
+
+    upd64 = mfma_roofline('chol_update', 'k_chol_update (f64 MFMA trailing update of the '
+                          'fp64 factorisations: chol(K), SYRK + chol of I + L_K^T W L_K)',
+                          PEAK_F64_MFMA_TFLOPS)
+    upd32 = mfma_roofline('chol_update32', 'k_chol_update32 (f32 MFMA trailing update of the '
+                          'mixed-precision Newton factorisation of B)', PEAK_F32_MFMA_TFLOPS)
+    # `roofline` is the kernel with the larger share of the step; the other one rides along
+    cands = [r for r in (upd64, upd32) if r is not None]
+    roofline = max(cands, key=lambda r: r['share_of_step_time'])
     extra = {}
+    for r, key in ((upd64, 'roofline_update_f64'), (upd32, 'roofline_update_f32')):
+        if r is not None and r is not roofline:
+            extra[key] = r
     gms, gcnt, gbytes = prof['gram']
     if gcnt:
         ach = gbytes / (gms * 1e-3) / 1e12
@@ -242,12 +257,14 @@ def main():
         'n_gpus': dist.world, 'steps': a.steps, 'warmup': a.warmup,
         'ms_per_step': 1e3 * elapsed / a.steps, 'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None, 'dtype': 'f64',
-        'dtype_detail': 'theta-path (Gram, Laplace/Newton, Cholesky factors) fp64 on f64 MFMA; '
+        'dtype_detail': 'theta-path Gram, chol(K) and the posterior-covariance factor fp64 on f64 '
+                        'MFMA; Newton matrix B factored in fp32 (f32 MFMA) with fp64 iterative '
+                        'refinement of each solve (mode = fp64 Newton mode to ~1e-12); '
                         'importance-sampling L.U fp32 on f32 MFMA; probit/LME epilogue fp32->fp64',
         'data': 'synthetic (X~N(0,1) normalised, y=sign of a GP prior draw; seed {0})'.format(a.seed),
         'config': {'workload': 'APM E-SS(u) + RD-SS(theta), ARD-SE probit GP classification, '
-                               'ApproxPosteriorIS estimator (BASELINE.json configs[3], per-GPU '
-                               'share of configs[4])',
+                               'ApproxPosteriorIS estimator, N=4096 D=32 N_imp=256 (BASELINE.json '
+                               'configs[2]; 64 chains per GPU = the per-GPU share of configs[3])',
                    'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'n_theta': P,
                    'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'

@@ -115,10 +115,12 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
 #define APM_PROF_GRAM 0
 #define APM_PROF_CHOL_UPDATE 1
 #define APM_PROF_UGEMM 2
-#define APM_PROF_NKINDS 3
+#define APM_PROF_CHOL_UPDATE32 3
+#define APM_PROF_NKINDS 4
 int apm_prof_enable(apm_ctx *ctx, int on);
 /* total device milliseconds and launch count per tracked kernel since the last reset; also the
- * algorithmic work: bytes (GRAM) or flops (CHOL_UPDATE, UGEMM) those launches performed */
+ * algorithmic work: bytes (GRAM) or flops (CHOL_UPDATE, CHOL_UPDATE32 = the fp32 Newton
+ * factorisation, UGEMM) those launches performed */
 int apm_prof_read(apm_ctx *ctx, int kind, double *total_ms, int64_t *launches, double *work,
                   int reset);
 

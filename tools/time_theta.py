@@ -34,7 +34,7 @@ for r in range(a.reps):
     t2 = time.perf_counter()
     print('rep {0}: theta-call {1:.2f} ms  u-call {2:.3f} ms  logf {3}  status {4}  ops {5}'
           .format(r, 1e3 * (t1 - t0), 1e3 * (t2 - t1), out[:2], st[:2], nops[:2]), flush=True)
-for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm')):
+for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32')):
     ms, cnt, wk = ctx.prof_read(k)
     rate = wk / (ms * 1e-3) if ms > 0 else 0
     print('{0:12s} total {1:9.3f} ms  launches {2:6d}  avg {3:8.4f} ms  {4:.3f} {5}/s'.format(
