@@ -35,18 +35,25 @@ void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet
 // panel rows [i0, R) minus the row tiles [glo, ghi) (pass glo = ghi = R for none)
 void launch_chol_panel(MatB A, int k, int i0, int R, int glo, int ghi, const double* Dinv,
                        int64_t dstride, Live live, int nchains, hipStream_t s);
+// Optional diag step fused into an update launch (the launch's tiles[0] is the diagonal tile
+// (d, d); Dinv / ldet / status are written as by launch_chol_diag for k = d).
+template <class TS>
+struct FusedDiag {
+    int enabled;
+    TS* Dinv;
+    int64_t dstride;
+    double* ldet;
+    int64_t lstride;
+    int fail_code;
+};
 // tiles: device list of packed (i << 16) | j built by build_update_tiles (super-tile order)
 // plus = true adds instead of subtracting (SYRK of the UL factorisation, postcov.hip)
-// lds_pad: extra dynamic LDS per workgroup (caps residency at 3 workgroups per CU, see capi.cpp)
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
-                        Live live, int nchains, hipStream_t s, int lds_pad = 0);
+                        Live live, int nchains, hipStream_t s,
+                        FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo = 0, int ghi = 0);
-// 128x128-per-workgroup variant for the rank-256 outer updates (list of 2x2 tile groups)
-void launch_chol_update_big(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int R,
-                            int jend, Live live, int nchains, hipStream_t s);
-std::vector<unsigned> build_update_tiles_big(int i0, int R, int j0, int jend);
 // one step (block J) of the backward solve L^T z = r, r stored in row `rrow` of A (in place),
 // z written to z[b*zstride + ...]
 void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,
@@ -60,7 +67,8 @@ void launch_chol_diag32(MatF A, int k, float* Dinv, int64_t dstride, double* lde
 void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const float* Dinv,
                          int64_t dstride, Live live, int nchains, hipStream_t s);
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                          int nchains, hipStream_t s);
+                          int nchains, hipStream_t s,
+                          FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0});
 struct NewtonVecs;
 void launch_form_B32(MatB K, MatF Bf, NewtonVecs v, int np, Live live, int nchains,
                      hipStream_t s);
@@ -72,6 +80,8 @@ void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride
 void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
                        int64_t vstride, Live live, int nchains, hipStream_t s);
 // refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
+void launch_refine_check(const double* x, const double* d, int64_t vstride, int np, double tol,
+                         int fail_code, Live live, int nchains, hipStream_t s);
 void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,
                    double* out, int64_t vstride, int np, Live live, int nchains, hipStream_t s);
 

@@ -33,10 +33,7 @@ struct ProfRec {
 struct apm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;     // panel stream of the one-panel lookahead (chol_range)
-    hipEvent_t ev_upd = nullptr, ev_pan = nullptr;
-    bool lookahead = false;  // APM_LOOKAHEAD=1: one-panel lookahead on stream2
-    int la_pad = 6400;  // 4 x (34816 + 6400) B > 160 KiB LDS per CU (APM_LA_PAD overrides)             // APM_LOOKAHEAD=0 disables (development knob)
+    bool fuse_diag = true;  // APM_FUSE_DIAG=0: stand-alone diag launches (development knob)
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
     double eps = 1e-8, tol = 1e-4;
@@ -52,6 +49,7 @@ struct apm_ctx {
     double* rvec = nullptr;   // 3 refinement vectors per chain (mixed-precision Newton)
     bool mixed = true;        // APM_MIXED=0: fp64 Newton factorisation (development knob)
     int n_refine = 1;         // APM_REFINE overrides
+    double refine_tol = 1e-3; // last correction / solution (max norms) accepted by the check
     int *active = nullptr, *status = nullptr, *n_iter = nullptr;
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;
     double *d_ca = nullptr, *d_cb = nullptr;
@@ -60,7 +58,6 @@ struct apm_ctx {
     SlotSet Sl{};
     UPool Up{};
     std::vector<void*> allocs;
-    bool big_update = false;
     bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix
     // profiling
     bool prof = false;
@@ -68,7 +65,7 @@ struct apm_ctx {
     size_t evnext = 0;
     std::vector<ProfRec> recs;
     // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
-    std::map<std::tuple<int, int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
+    std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
 };
 
 namespace {
@@ -169,13 +166,11 @@ double update_flops(int i0, int R, int j0, int jend, int kc, Gap g) {
     return f;
 }
 
-std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g,
-                                    bool big) {
-    auto key = std::make_tuple(i0, R, j0, jend, (int)big, g.lo, g.hi);
+std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g) {
+    auto key = std::make_tuple(i0, R, j0, jend, g.lo, g.hi);
     auto it = c->tile_lists.find(key);
     if (it != c->tile_lists.end()) return it->second;
-    std::vector<unsigned> v = big ? build_update_tiles_big(i0, R, j0, jend)
-                                  : build_update_tiles(i0, R, j0, jend, g.lo, g.hi);
+    std::vector<unsigned> v = build_update_tiles(i0, R, j0, jend, g.lo, g.hi);
     unsigned* d = dalloc<unsigned>(c, v.size());
     HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
     auto val = std::make_pair(d, (int)v.size());
@@ -183,75 +178,55 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
     return val;
 }
 
+// Trailing update of tiles (i, j), i in [i0, R) minus the gap, j in [j0, min(i, jend-1)], by
+// columns [k0, k0+kc). fuse_k >= 0: the launch also factors diagonal tile (fuse_k, fuse_k), which
+// must be its first tile (i0 == j0 == fuse_k; the super-tile order starts there).
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
-                    bool plus, int count, hipStream_t s = nullptr, int lds_pad = 0) {
-    if (!s) s = c->stream;
+                    bool plus, int count, int fuse_k = -1, int fail_code = 0) {
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
-    // wide updates (outer, rank 256) may use the 128x128 kernel; narrow inner ones the 64x64 one
-    const bool big = c->big_update && !plus && g.hi <= g.lo && kc > 1 && (jend - j0) >= 4;
-    const auto tl = tile_list(c, i0, R, j0, jend, g, big);
+    const auto tl = tile_list(c, i0, R, j0, jend, g);
     if (tl.second <= 0) return;
+    FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
+    if (fuse_k >= 0) fd = FusedDiag<double>{1, c->Dinv, c->dstride, c->ldet, c->lstride, fail_code};
     ProfScope ps(c, APM_PROF_CHOL_UPDATE,
-                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0, s);
-    if (big)
-        launch_chol_update_big(M, k0, kc, tl.first, tl.second, R, jend, live_of(c), count, s);
-    else
-        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, s, lds_pad);
+                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0);
+    launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream, fd);
     check_launch();
 }
 
-// Tile columns [K, Kend) of one outer panel: 64-wide diag / panel / inner-update steps on stream s.
-void factor_panel(apm_ctx* c, MatB M, int K, int Kend, int R, int fail_code, int count,
-                  bool factor_diag, int row_start, GapFn gap, hipStream_t s) {
-    const Live lv = live_of(c);
-    for (int k = K; k < Kend; ++k) {
-        if (factor_diag) {
-            launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code, count,
-                             s);
-            check_launch();
-        }
-        const Gap g = gap(k, c->nb);
-        launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv, c->dstride, lv,
-                          count, s);
-        check_launch();
-        tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false, count, s);
-    }
-}
-
-// One-panel lookahead: the outer update of panel K is split into the next panel's columns
-// [Kend, Kn) and the rest [Kn, Cb). The next panel is factored on stream2 (high priority) as soon
-// as its columns are updated, concurrently with the bulk update on the main stream; the two touch
-// disjoint tile columns and read only the finished panel K. The latency-bound diag/panel chain
-// (one 64-thread workgroup per chain) thus hides under the MFMA-bound rank-256 update.
+// Two-level right-looking Cholesky over tile columns [k0, k1) of rows < R (tile units), the
+// trailing matrix spanning columns < Cb. Outer panels of OUTER tiles (256 columns) are factored
+// with 64-wide diag / panel / inner-update steps; the rest of the matrix then receives one
+// rank-256 update per outer panel (4x less read-modify-write traffic than rank-64 steps). Every
+// diagonal tile after the first is factored inside the update launch that completes it (fused
+// diag: its one-wave latency hides under that launch instead of idling the GPU between launches).
+// row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
+// augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
 void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
                 bool factor_diag = true, int row_start = 0, GapFn gap = no_gap) {
-    hipStream_t s1 = c->stream, s2 = c->stream2;
-    factor_panel(c, M, k0, std::min(k0 + OUTER, k1), R, fail_code, count, factor_diag, row_start,
-                 gap, s1);
+    const Live lv = live_of(c);
+    const bool fuse = factor_diag && c->fuse_diag && row_start <= k0;
+    bool have_diag = false;  // tile (k, k) already factored by the previous update launch
     for (int K = k0; K < k1; K += OUTER) {
-        const int Kend = std::min(K + OUTER, k1), Kn = std::min(Kend + OUTER, k1);
-        const int i0 = std::max(Kend, row_start);
-        const Gap g = gap(Kend - 1, c->nb);
-        if (Kend >= k1) {  // rows beyond the factored range (e.g. the RHS block) only
-            tracked_update(c, M, K, Kend - K, i0, R, Kend, Cb, g, false, count, s1);
-            break;
+        const int Kend = std::min(K + OUTER, k1);
+        for (int k = K; k < Kend; ++k) {
+            if (factor_diag && !have_diag) {
+                launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
+                                 count, c->stream);
+                check_launch();
+            }
+            const Gap g = gap(k, c->nb);
+            launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv,
+                              c->dstride, lv, count, c->stream);
+            check_launch();
+            have_diag = fuse && k + 1 < Kend;
+            tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false,
+                           count, have_diag ? k + 1 : -1, fail_code);
         }
-        if (!c->lookahead) {
-            tracked_update(c, M, K, Kend - K, i0, R, Kend, Cb, g, false, count, s1);
-            factor_panel(c, M, Kend, Kn, R, fail_code, count, factor_diag, row_start, gap, s1);
-            continue;
-        }
-        tracked_update(c, M, K, Kend - K, i0, R, Kend, Kn, g, false, count, s1);
-        HIPC(hipEventRecord(c->ev_upd, s1));
-        HIPC(hipStreamWaitEvent(s2, c->ev_upd, 0));
-        factor_panel(c, M, Kend, Kn, R, fail_code, count, factor_diag, row_start, gap, s2);
-        HIPC(hipEventRecord(c->ev_pan, s2));
-        // padded to 3 resident workgroups per CU (measured as fast as 4): every CU keeps room
-        // for one diag / panel / inner-update workgroup of the panel stream
-        tracked_update(c, M, K, Kend - K, std::max(Kn, row_start), R, Kn, Cb, g, false, count, s1,
-                       c->la_pad);
-        HIPC(hipStreamWaitEvent(s1, c->ev_pan, 0));
+        have_diag = fuse && Kend < k1;
+        tracked_update(c, M, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb,
+                       gap(Kend - 1, c->nb), false, count, have_diag ? Kend : -1, fail_code);
     }
 }
 
@@ -262,31 +237,43 @@ MatF b32_of(apm_ctx* c) {
 float* dinv32_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv); }
 
 void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
-                      int count) {
+                      int count, int fuse_k = -1, int fail_code = 0) {
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
-    const auto tl = tile_list(c, i0, R, j0, jend, Gap{0, 0}, false);
+    const auto tl = tile_list(c, i0, R, j0, jend, Gap{0, 0});
     if (tl.second <= 0) return;
+    FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
+    if (fuse_k >= 0)
+        fd = FusedDiag<float>{1, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, fail_code};
     ProfScope ps(c, APM_PROF_CHOL_UPDATE32,
                  c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * count : 0.0);
-    launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream);
+    launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd);
     check_launch();
 }
 
+// chol_range's twin for the fp32 Newton matrix (same steps, same fused diag)
 void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_code, int count) {
     const Live lv = live_of(c);
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
+    bool have_diag = false;
     for (int K = k0; K < k1; K += OUTER) {
         const int Kend = std::min(K + OUTER, k1);
         for (int k = K; k < Kend; ++k) {
-            launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count, c->stream);
-            check_launch();
+            if (!have_diag) {
+                launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
+                                   c->stream);
+                check_launch();
+            }
             launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
             check_launch();
-            tracked_update32(c, M, k, 1, k + 1, R, k + 1, Kend, count);
+            have_diag = c->fuse_diag && k + 1 < Kend;
+            tracked_update32(c, M, k, 1, k + 1, R, k + 1, Kend, count, have_diag ? k + 1 : -1,
+                             fail_code);
         }
-        tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count);
+        have_diag = c->fuse_diag && Kend < k1;
+        tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
+                         fail_code);
     }
 }
 
@@ -337,6 +324,10 @@ void newton_solve32(apm_ctx* c, int count) {
         }
         for (int J = nb - 1; J >= 0; --J) {
             launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lv, count, s);
+            check_launch();
+        }
+        if (it + 1 == c->n_refine) {  // accept only a converged refinement (else: fp64 rerun)
+            launch_refine_check(c->v.z, r3, vs, np, c->refine_tol, APM_STATUS_CHOL_B, lv, count, s);
             check_launch();
         }
         launch_refine(2, nullptr, nullptr, c->v.z, nullptr, r3, vs, np, lv, count, s);  // x += d
@@ -543,20 +534,14 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t ldx, const double* y, double eps, int64_t S, int64_t max_batch,
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
-    if (const char* e = getenv("APM_BIG_UPDATE")) c->big_update = atoi(e) != 0;
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
     if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
     HIPC(hipSetDevice(device));
-    if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
-    if (const char* e = getenv("APM_LA_PAD")) c->la_pad = std::max(0, atoi(e));
+    if (const char* e = getenv("APM_FUSE_DIAG")) c->fuse_diag = atoi(e) != 0;
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
+    if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    int prio_lo = 0, prio_hi = 0;
-    HIPC(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    HIPC(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_hi));
-    HIPC(hipEventCreateWithFlags(&c->ev_upd, hipEventDisableTiming));
-    HIPC(hipEventCreateWithFlags(&c->ev_pan, hipEventDisableTiming));
     c->kind = kind;
     c->n = (int)n;
     c->d = (int)d;
@@ -626,10 +611,6 @@ void free_ctx(apm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
-    if (c->ev_upd) (void)hipEventDestroy(c->ev_upd);
-    if (c->ev_pan) (void)hipEventDestroy(c->ev_pan);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -9,52 +9,12 @@
 #include <vector>
 
 #include "apm_internal.h"
+#include "diag.h"
 
 // v_mfma_f64_16x16x4_f64 operand/result maps (cdna_hip_programming.md §3):
 //   A: lane l holds A[row = l&15][k = l>>4]; B: lane l holds B[k = l>>4][col = l&15]
 //   C/D: lane l, reg r  ->  row = (l>>4) + 4r, col = l&15
 #define F64_CROW(l, r) (((l) >> 4) + 4 * (r))
-
-// acc += (NEG ? -1 : 1) * A[64x64] * B[64x64]^T restricted to this wave's quadrant (wr, wc).
-// Both operands are row-major [output index][inner index]. The inner index is permuted per lane
-// (lane group kq handles inner k = 16*kq + t at MFMA step t) so that each lane streams 16
-// contiguous doubles (128 B) per operand row with 16-byte loads; the permutation is the same for
-// A and B, so the sum over the inner index is unchanged.
-template <bool NEG>
-__device__ __forceinline__ void tile_nt_f64(d4_t (&acc)[2][2], const double* __restrict__ A,
-                                            int64_t lda, const double* __restrict__ B,
-                                            int64_t ldb, int wr, int wc, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-    double a[2][16], b[2][16];
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi) {
-        const double* p = A + (int64_t)(32 * wr + 16 * bi + r16) * lda + kq * 16;
-#pragma unroll
-        for (int t = 0; t < 16; t += 2) {
-            const d2_t v = *reinterpret_cast<const d2_t*>(p + t);
-            a[bi][t] = NEG ? -v.x : v.x;
-            a[bi][t + 1] = NEG ? -v.y : v.y;
-        }
-    }
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
-        const double* p = B + (int64_t)(32 * wc + 16 * bj + r16) * ldb + kq * 16;
-#pragma unroll
-        for (int t = 0; t < 16; t += 2) {
-            const d2_t v = *reinterpret_cast<const d2_t*>(p + t);
-            b[bj][t] = v.x;
-            b[bj][t + 1] = v.y;
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t)
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj)
-                acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi][t], b[bj][t],
-                                                                    acc[bi][bj], 0, 0, 0);
-}
 
 __device__ __forceinline__ void tile_acc_load(d4_t (&acc)[2][2], const double* T, int64_t ld,
                                               int wr, int wc, int lane) {
@@ -211,123 +171,19 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 }
 
 // ------------------------------------------------------------------------------- diagonal tile
-#ifdef APM_DIAG_STAMPS
-__device__ unsigned long long g_diag_stamps[16];  // diagnostic build only (tools/diag_stamps.cpp)
-#endif
-#define DP 65  // LDS pitch (doubles) of the diag kernel's tile
-
-// Broadcast lane l's value of a wave-uniform-indexed register (v_readlane x2).
-__device__ __forceinline__ double rdlane(double v, int l) {
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
-// 16x16x16 products on LDS operands with one v_mfma_f64_16x16x4_f64 chain (4 steps):
-//   NT: acc[r][c] += sum_k A[r][k] * B[c][k]      NN: acc[r][c] += sum_k A[r][k] * B[k][c]
-template <bool NEG>
-__device__ __forceinline__ void mm16_nt(d4_t& acc, const double* a, int lda, const double* b,
-                                        int ldb, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const double av = a[r16 * lda + 4 * t + kq];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -av : av, b[r16 * ldb + 4 * t + kq], acc,
-                                                   0, 0, 0);
-    }
-}
-__device__ __forceinline__ void mm16_nn(d4_t& acc, const double* a, int lda, const double* b,
-                                        int ldb, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
-                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
-}
-__device__ __forceinline__ void st16(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dst[((lane >> 4) + 4 * q) * ld + (lane & 15)] = sgn * acc[q];
-}
-__device__ __forceinline__ void st16t(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dst[(lane & 15) * ld + (lane >> 4) + 4 * q] = sgn * acc[q];
-}
-// Products with a diagonal block X of the inverse held as (strict lower part transposed at Td,
-// diagonal in xd): X[r][c] = c < r ? Td[c][r] : (c == r ? xd[r] : 0).
-__device__ __forceinline__ double xblk(const double* Td, const double* xd, int r, int c) {
-    return (c < r) ? Td[c * DP + r] : ((c == r) ? xd[r] : 0.0);
-}
-//   acc += A * X^T
-__device__ __forceinline__ void mm16_nt_xb(d4_t& acc, const double* a, int lda, const double* Td,
-                                           const double* xd, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
-                                                   xblk(Td, xd, r16, 4 * t + kq), acc, 0, 0, 0);
-}
-//   acc += A * X
-__device__ __forceinline__ void mm16_nn_xb(d4_t& acc, const double* a, int lda, const double* Td,
-                                           const double* xd, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
-                                                   xblk(Td, xd, 4 * t + kq, r16), acc, 0, 0, 0);
-}
-//   acc += X * B
-__device__ __forceinline__ void mm16_nn_xa(d4_t& acc, const double* Td, const double* xd,
-                                           const double* b, int ldb, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xblk(Td, xd, r16, 4 * t + kq),
-                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
-}
-__device__ __forceinline__ void ld16(d4_t& acc, const double* src, int ld, int lane) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = src[((lane >> 4) + 4 * q) * ld + (lane & 15)];
-}
-
-// 64x64 Cholesky + inverse of the lower factor by ONE wave (no barriers), blocked by 16:
-// per 16-column block the 16x16 diagonal block is factored with lane r holding row r in
-// registers (pivot by v_readlane, column broadcast through LDS, 1/sqrt by v_rsq_f64 + two Newton
-// steps) and inverted (lane c substitutes column c); the 16-wide panel solve, the rank-16
-// trailing update and the assembly of the full inverse X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb are
-// 16x16x16 f64-MFMA products on LDS operands. The inverse is kept transposed in the unused upper
-// triangle of T (X_ab, a > b, in block (b, a); the strictly lower part of X_aa in the upper part of
-// diagonal block (a, a); its diagonal in xdg): 36 KB of LDS, so that the kernel fits next to three
-// padded update workgroups on a CU (lookahead, capi.cpp).
-// Storage of the tile and of Dinv is fp64 (MatB) or fp32 (MatF, the mixed-precision Newton
-// factorisation, chol32.hip); the factorisation itself always runs in fp64.
-__device__ __forceinline__ d2_t ld2(const double* p) { return *reinterpret_cast<const d2_t*>(p); }
-__device__ __forceinline__ d2_t ld2(const float* p) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    return d2_t{(double)v.x, (double)v.y};
-}
+// Stand-alone diag step (one wave per chain): tile (k, k) -> LDS, diag_factor (diag.h). Used for
+// the first column of every factorisation; every later diagonal tile is factored inside the
+// update launch that produces it (k_chol_update below, fuse_diag).
 template <class Mat, class TS>
 __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_t dstride,
                                                   double* ldet, int64_t lstride, Live live,
                                                   int fail_code) {
     const int b = blockIdx.x;
     if (!chain_live(live, b)) return;
-    __shared__ double T[64 * DP];
-    __shared__ double xdg[64];
-    __shared__ double Tmp[16 * 17];
-    __shared__ double colb[16];
-    __shared__ double dg[64];
+    __shared__ DiagSmem S;
     const int lane = threadIdx.x;
-#ifdef APM_DIAG_STAMPS
-    unsigned long long stamps[16];
-    int ns = 0;
-#define STAMP() if (lane == 0 && ns < 16) stamps[ns++] = __builtin_amdgcn_s_memtime()
-#else
-#define STAMP()
-#endif
-    STAMP();
     TS* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
-    // 32 KB tile -> LDS: 4 rounds of 8 independent 16-byte loads per lane (lane covers 2 columns)
+    // 64x64 tile -> LDS: 4 rounds of 8 independent 2-element loads per lane (lane: 2 columns)
 #pragma unroll
     for (int q0 = 0; q0 < 64; q0 += 16) {
         d2_t v[8];
@@ -339,107 +195,12 @@ __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const int q = q0 + 2 * h + (lane >> 5);
-            T[q * DP + 2 * (lane & 31)] = v[h].x;
-            T[q * DP + 2 * (lane & 31) + 1] = v[h].y;
+            S.T[q * DP + 2 * (lane & 31)] = v[h].x;
+            S.T[q * DP + 2 * (lane & 31) + 1] = v[h].y;
         }
     }
-    STAMP();
-    const int r = lane & 15;
-    for (int kb = 0; kb < 4; ++kb) {
-        const int o = kb * 16;
-        // (a) factor the 16x16 diagonal block
-        double row[16], yv[16], dv[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) row[c] = T[(o + r) * DP + o + c];
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const double p = rdlane(row[j], j);
-            bad |= !(p > 0.0);
-            double y = __builtin_amdgcn_rsq(p);
-            y = y * (1.5 - 0.5 * p * y * y);
-            y = y * (1.5 - 0.5 * p * y * y);
-            yv[j] = y;
-            dv[j] = p * y;
-            row[j] = (r > j) ? row[j] * y : ((r == j) ? dv[j] : row[j]);
-            if (lane < 16) colb[r] = row[j];
-#pragma unroll
-            for (int c = j + 1; c < 16; ++c) row[c] -= row[j] * colb[c];
-        }
-        if (bad) {  // wave-uniform
-            if (lane == 0) live.status[b] = fail_code;
-            return;
-        }
-        if (lane < 16) {
-#pragma unroll
-            for (int c = 0; c < 16; ++c) T[(o + r) * DP + o + c] = (c <= r) ? row[c] : 0.0;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) dg[o + j] = dv[j];
-        }
-        // inverse of the 16x16 factor: lane c (< 16) solves for column c
-        {
-            const int c = r;
-            double x[16];
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
-                double sacc = (rr == c) ? 1.0 : 0.0;
-#pragma unroll
-                for (int m = 0; m < rr; ++m) sacc -= T[(o + rr) * DP + o + m] * x[m];
-                x[rr] = (rr >= c) ? sacc * yv[rr] : 0.0;
-            }
-            if (lane < 16) {
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr)
-                    if (rr > c) T[(o + c) * DP + o + rr] = x[rr];
-                xdg[o + c] = x[c];
-            }
-        }
-        if (kb == 3) break;
-        // (b) panel: T[ib][kb] = T[ib][kb] * inv(L_kb,kb)^T for the blocks below
-        for (int ib = kb + 1; ib < 4; ++ib) {
-            d4_t acc = {0.0, 0.0, 0.0, 0.0};
-            mm16_nt_xb(acc, &T[(16 * ib) * DP + o], DP, &T[o * DP + o], &xdg[o], lane);
-            st16(acc, &T[(16 * ib) * DP + o], DP, lane, 1.0);
-        }
-        // (c) rank-16 trailing update of the lower blocks
-        for (int ib = kb + 1; ib < 4; ++ib)
-            for (int jb = kb + 1; jb <= ib; ++jb) {
-                d4_t acc;
-                ld16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane);
-                mm16_nt<true>(acc, &T[(16 * ib) * DP + o], DP, &T[(16 * jb) * DP + o], DP, lane);
-                st16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane, 1.0);
-            }
-        STAMP();
-    }
-    // off-diagonal blocks of the inverse, block row by block row
-    for (int a = 1; a < 4; ++a)
-        for (int bb = 0; bb < a; ++bb) {
-            d4_t acc = {0.0, 0.0, 0.0, 0.0};
-            mm16_nn_xb(acc, &T[(16 * a) * DP + 16 * bb], DP, &T[(16 * bb) * DP + 16 * bb],
-                       &xdg[16 * bb], lane);
-            for (int kk = bb + 1; kk < a; ++kk)  // X_kk,bb is stored transposed at T block (bb, kk)
-                mm16_nt<false>(acc, &T[(16 * a) * DP + 16 * kk], DP, &T[(16 * bb) * DP + 16 * kk],
-                               DP, lane);
-            st16(acc, Tmp, 17, lane, 1.0);
-            d4_t acc2 = {0.0, 0.0, 0.0, 0.0};
-            mm16_nn_xa(acc2, &T[(16 * a) * DP + 16 * a], &xdg[16 * a], Tmp, 17, lane);
-            st16t(acc2, &T[(16 * bb) * DP + 16 * a], DP, lane, -1.0);
-        }
-    STAMP();
-    TS* D = Dinv + b * dstride + (int64_t)k * 4096;
-    for (int q = 0; q < 64; ++q) {
-        At[(int64_t)q * A.ld + lane] = (TS)((lane <= q) ? T[q * DP + lane] : 0.0);
-        D[q * 64 + lane] = (TS)((lane < q) ? T[lane * DP + q] : ((lane == q) ? xdg[q] : 0.0));
-    }
-    const double l = wave_sum_d(log(dg[lane]));
-    if (lane == 0) ldet[b * lstride + k] = l;
-#ifdef APM_DIAG_STAMPS
-    STAMP();
-    if (lane == 0 && k == 0 && b == 0)
-        for (int q = 0; q < ns; ++q) g_diag_stamps[q] = stamps[q] - stamps[0];
-#endif
+    diag_factor<TS>(S, At, A.ld, Dinv + b * dstride + (int64_t)k * 4096, ldet + b * lstride + k,
+                    live.status + b, fail_code, lane);
 }
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
@@ -511,182 +272,78 @@ __device__ __forceinline__ long xcd_remap(long L, long total) {
     return base + (L >> 3);
 }
 
+// Fused diag (fd.enabled): tiles[0] must be the diagonal tile (d, d) the next column step
+// factors. Workgroups 0 .. nchains-1 (dispatched first) update chain b's tile (d, d), keep it in
+// LDS and factor it with wave 0 (diag_factor), so its latency hides under the rest of the launch;
+// the other workgroups take the remaining (ntiles - 1) tiles of every chain.
 __global__ __launch_bounds__(256, UPD_WPE) void k_chol_update(MatB A, int k0, int kc,
-                                                     const unsigned* __restrict__ tiles, int ntiles,
-                                                     int nchains, int plus, Live live) {
-    const long total = (long)ntiles * nchains;
+                                                              const unsigned* __restrict__ tiles,
+                                                              int ntiles, int nchains, int plus,
+                                                              Live live, FusedDiag<double> fd) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
-    __shared__ GemmSmem sm;
-    {
-        const long L = blockIdx.x;
-        const long w = xcd_remap(L, total);
-        const int b = (int)(w / ntiles);
-        if (!chain_live(live, b)) return;
-        const unsigned ij = tiles[w % ntiles];
-        const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
-        double* Ab = A.base + b * A.cstride;
-        double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
-        d4_t acc[2][2];
+    __shared__ union {
+        GemmSmem g;
+        DiagSmem d;
+    } sm;
+    int b, t;
+    const bool fused = fd.enabled && (int)blockIdx.x < nchains;
+    if (fused) {
+        b = blockIdx.x;
+        t = 0;
+    } else {
+        const int nt = fd.enabled ? ntiles - 1 : ntiles;
+        const long L = (long)blockIdx.x - (fd.enabled ? nchains : 0);
+        const long w = xcd_remap(L, (long)nt * nchains);
+        b = (int)(w / nt);
+        t = (int)(w % nt) + (fd.enabled ? 1 : 0);
+    }
+    if (!chain_live(live, b)) return;
+    const unsigned ij = tiles[t];
+    const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
+    double* Ab = A.base + b * A.cstride;
+    double* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
+    d4_t acc[2][2];
 #if UPD_LATEC
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
-        const double* Cold = Aij;
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
+    const double* Cold = Aij;
 #else
-        tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
-        const double* Cold = nullptr;
+    tile_acc_load(acc, Aij, A.ld, wr, wc, lane);
+    const double* Cold = nullptr;
 #endif
-        const double* Ai = Ab + (int64_t)(i * 64) * A.ld + k0 * 64;
-        const double* Aj = Ab + (int64_t)(j * 64) * A.ld + k0 * 64;
-        if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
-            tile_gemm_nt<false>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm, Cold, A.ld);
-        else
-            tile_gemm_nt<true>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm, Cold, A.ld);
+    const double* Ai = Ab + (int64_t)(i * 64) * A.ld + k0 * 64;
+    const double* Aj = Ab + (int64_t)(j * 64) * A.ld + k0 * 64;
+    if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
+        tile_gemm_nt<false>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm.g, Cold, A.ld);
+    else
+        tile_gemm_nt<true>(acc, Ai, A.ld, Aj, A.ld, 64 * kc, sm.g, Cold, A.ld);
+    if (!fused) {
         tile_acc_store(acc, Aij, A.ld, wr, wc, lane);
+        return;
     }
+    // tile_gemm_nt ended on a barrier: the GEMM staging area is free for the diag working set
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sm.d.T[(32 * wr + 16 * bi + F64_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
+                       (lane & 15)] = acc[bi][bj][r];
+    __syncthreads();
+    if (wv != 0) return;
+    diag_factor<double>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
+                        fd.ldet + b * fd.lstride + i, live.status + b, fd.fail_code, lane);
 }
 
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
-                        Live live, int nchains, hipStream_t s, int lds_pad) {
+                        Live live, int nchains, hipStream_t s, FusedDiag<double> fd) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), lds_pad, s, A, k0, kc,
-                       tiles, ntiles, nchains, (int)plus, live);
-}
-
-// ------------------------------------------------------------------------------- 128x128 update
-// Outer (rank-256) updates: one workgroup per 2x2 group of 64-tiles; wave (wr, wc) owns sub-tile
-// (i+wr, j+wc) as 4x4 v_mfma_f64_16x16x4 accumulators (128 VGPRs), so each 16-deep LDS slice
-// feeds 64 MFMAs per wave from 8 fragment reads (twice the operand reuse of the 64x64 kernel).
-// Sub-tiles outside the update region (above the diagonal, past R or jend) skip their MFMAs and
-// stores; out-of-range operand rows are clamped to a valid row and their results discarded.
-struct BigSmem {
-    double a[2][128][17];
-    double b[2][128][17];
-};
-
-__global__ __launch_bounds__(256, 2) void k_chol_update_big(MatB A, int k0, int kc,
-                                                         const unsigned* __restrict__ tiles,
-                                                         int ntiles, int nchains, int R, int jend,
-                                                         Live live) {
-    const long total = (long)ntiles * nchains;
-    const long w = xcd_remap(blockIdx.x, total);
-    const int b = (int)(w / ntiles);
-    if (!chain_live(live, b)) return;
-    const unsigned ij = tiles[w % ntiles];
-    const int i0 = (int)(ij >> 16), j0 = (int)(ij & 0xffff);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
-    const int r16 = lane & 15, kq = lane >> 4;
-    const int ti = i0 + wr, tj = j0 + wc;
-    const bool valid = ti < R && tj < jend && tj <= ti;
-    double* Ab = A.base + b * A.cstride;
-    __shared__ BigSmem sm;
-    d4_t acc[4][4];
-    double* Aij = Ab + (int64_t)(ti * 64) * A.ld + tj * 64;
-    if (valid) {
-#pragma unroll
-        for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[bi][bj][q] = Aij[(int64_t)(16 * bi + F64_CROW(lane, q)) * A.ld + 16 * bj + r16];
-    }
-    // staging: 1024 pieces of 16 B per operand slice (128 rows x 128 B); thread -> 4 pieces
-    const int pc = (tid & 7) * 2;
-    const double* pa[4];
-    const double* pb[4];
-    int prow[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int row = (tid >> 3) + 32 * h;  // 0..127
-        prow[h] = row;
-        const int ra = min(i0 * 64 + row, R * 64 - 1);
-        const int rb = min(j0 * 64 + row, R * 64 - 1);
-        pa[h] = Ab + (int64_t)ra * A.ld + k0 * 64 + pc;
-        pb[h] = Ab + (int64_t)rb * A.ld + k0 * 64 + pc;
-    }
-    d2_t ra_[4], rb_[4];
-    const int nsub = 4 * kc;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        ra_[h] = *reinterpret_cast<const d2_t*>(pa[h]);
-        rb_[h] = *reinterpret_cast<const d2_t*>(pb[h]);
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        sm.a[0][prow[h]][pc] = -ra_[h].x;
-        sm.a[0][prow[h]][pc + 1] = -ra_[h].y;
-        sm.b[0][prow[h]][pc] = rb_[h].x;
-        sm.b[0][prow[h]][pc + 1] = rb_[h].y;
-    }
-    __syncthreads();
-    for (int sl = 0; sl < nsub; ++sl) {
-        const int cur = sl & 1;
-        if (sl + 1 < nsub) {
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                ra_[h] = *reinterpret_cast<const d2_t*>(pa[h] + (sl + 1) * 16);
-                rb_[h] = *reinterpret_cast<const d2_t*>(pb[h] + (sl + 1) * 16);
-            }
-        }
-        if (valid) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                double av[4], bv[4];
-#pragma unroll
-                for (int bi = 0; bi < 4; ++bi) av[bi] = sm.a[cur][64 * wr + 16 * bi + r16][4 * t + kq];
-#pragma unroll
-                for (int bj = 0; bj < 4; ++bj) bv[bj] = sm.b[cur][64 * wc + 16 * bj + r16][4 * t + kq];
-#pragma unroll
-                for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-                    for (int bj = 0; bj < 4; ++bj)
-                        acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[bi], bv[bj],
-                                                                            acc[bi][bj], 0, 0, 0);
-            }
-        }
-        if (sl + 1 < nsub) {
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                sm.a[cur ^ 1][prow[h]][pc] = -ra_[h].x;
-                sm.a[cur ^ 1][prow[h]][pc + 1] = -ra_[h].y;
-                sm.b[cur ^ 1][prow[h]][pc] = rb_[h].x;
-                sm.b[cur ^ 1][prow[h]][pc + 1] = rb_[h].y;
-            }
-        }
-        __syncthreads();
-    }
-    if (valid) {
-#pragma unroll
-        for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    Aij[(int64_t)(16 * bi + F64_CROW(lane, q)) * A.ld + 16 * bj + r16] = acc[bi][bj][q];
-    }
-}
-
-void launch_chol_update_big(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int R,
-                            int jend, Live live, int nchains, hipStream_t s) {
-    if (ntiles <= 0) return;
-    const long total = (long)ntiles * nchains;
-    hipLaunchKernelGGL(k_chol_update_big, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, R, jend, live);
-}
-
-// Host: 2x2 groups (top-left tile (i, j)) covering the update region, in super-tile order
-std::vector<unsigned> build_update_tiles_big(int i0, int R, int j0, int jend) {
-    std::vector<unsigned> v;
-    const int S = 8;
-    for (int I = i0; I < R; I += S)
-        for (int J = j0; J < jend; J += S)
-            for (int i = I; i < std::min(I + S, R); i += 2)
-                for (int j = J; j < std::min(J + S, jend); j += 2)
-                    if (j <= i + 1) v.push_back(((unsigned)i << 16) | (unsigned)j);
-    return v;
+    hipLaunchKernelGGL(k_chol_update, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
+                       ntiles, nchains, (int)plus, live, fd);
 }
 
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,

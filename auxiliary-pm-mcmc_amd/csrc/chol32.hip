@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "apm_internal.h"
+#include "diag.h"
 
 #define KS32 32          // slice depth (floats) of the LDS-staged tile GEMM
 #define LP32 (KS32 + 2)  // pitch 34 floats: fragment reads (16 rows x 4 k) hit 32 distinct banks
@@ -173,35 +174,65 @@ __device__ __forceinline__ long xcd_remap32(long L, long total) {
     return base + (L >> 3);
 }
 
+// fd.enabled: workgroups 0 .. nchains-1 update the diagonal tile tiles[0] = (d, d) of chain b and
+// factor it in place (diag_factor, fp64 arithmetic, fp32 storage) - see k_chol_update (chol.hip).
 __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
                                                        const unsigned* __restrict__ tiles,
-                                                       int ntiles, int nchains, Live live) {
-    const long total = (long)ntiles * nchains;
-    const long w = xcd_remap32(blockIdx.x, total);
-    const int b = (int)(w / ntiles);
+                                                       int ntiles, int nchains, Live live,
+                                                       FusedDiag<float> fd) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
+    __shared__ union {
+        GemmSmem32 g;
+        DiagSmem d;
+    } sm;
+    int b, t;
+    const bool fused = fd.enabled && (int)blockIdx.x < nchains;
+    if (fused) {
+        b = blockIdx.x;
+        t = 0;
+    } else {
+        const int nt = fd.enabled ? ntiles - 1 : ntiles;
+        const long L = (long)blockIdx.x - (fd.enabled ? nchains : 0);
+        const long w = xcd_remap32(L, (long)nt * nchains);
+        b = (int)(w / nt);
+        t = (int)(w % nt) + (fd.enabled ? 1 : 0);
+    }
     if (!live32(live, b)) return;
-    const unsigned ij = tiles[w % ntiles];
+    const unsigned ij = tiles[t];
     const int i = (int)(ij >> 16), j = (int)(ij & 0xffff);
     float* Ab = A.base + b * A.cstride;
     float* Aij = Ab + (int64_t)(i * 64) * A.ld + j * 64;
-    __shared__ GemmSmem32 sm;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     f4_t acc[2][2];
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
     tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
-                         Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm, Aij, A.ld);
-    tile32_store(acc, Aij, A.ld, wr, wc, lane);
+                         Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm.g, Aij, A.ld);
+    if (!fused) {
+        tile32_store(acc, Aij, A.ld, wr, wc, lane);
+        return;
+    }
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sm.d.T[(32 * wr + 16 * bi + F32_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
+                       (lane & 15)] = (double)acc[bi][bj][r];
+    __syncthreads();
+    if (wv != 0) return;
+    diag_factor<float>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
+                       fd.ldet + b * fd.lstride + i, live.status + b, fd.fail_code, lane);
 }
 
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                          int nchains, hipStream_t s) {
+                          int nchains, hipStream_t s, FusedDiag<float> fd) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, live);
+                       ntiles, nchains, live, fd);
 }
 
 // ------------------------------------------------------------------------------- B in fp32
@@ -369,6 +400,41 @@ __global__ __launch_bounds__(256) void k_refine(int mode, const double* __restri
         x[o] += out[o];
     else
         out[o] = 0.0;
+}
+
+// Acceptance test of the refined solve: the last correction d must be small against x
+// (max|d| <= tol * max|x|; the refined error is then ~ (tol)^2 relative). Otherwise the fp32
+// factor is too inaccurate for this chain (extreme theta) and status = fail_code sends the chain
+// to the fp64 rerun (capi.cpp newton_is).
+__global__ __launch_bounds__(256) void k_refine_check(const double* __restrict__ x,
+                                                      const double* __restrict__ d,
+                                                      int64_t vstride, int np, double tol,
+                                                      int fail_code, Live live) {
+    const int b = blockIdx.x;
+    if (!live32(live, b)) return;
+    double mx = 0.0, md = 0.0;
+    for (int i = threadIdx.x; i < np; i += 256) {
+        mx = fmax(mx, fabs(x[b * vstride + i]));
+        md = fmax(md, fabs(d[b * vstride + i]));
+    }
+    __shared__ double sx[256], sd[256];
+    sx[threadIdx.x] = mx;
+    sd[threadIdx.x] = md;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            sx[threadIdx.x] = fmax(sx[threadIdx.x], sx[threadIdx.x + h]);
+            sd[threadIdx.x] = fmax(sd[threadIdx.x], sd[threadIdx.x + h]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && !(sd[0] <= tol * sx[0])) live.status[b] = fail_code;
+}
+
+void launch_refine_check(const double* x, const double* d, int64_t vstride, int np, double tol,
+                         int fail_code, Live live, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_refine_check, dim3(nchains), dim3(256), 0, s, x, d, vstride, np, tol,
+                       fail_code, live);
 }
 
 void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,

@@ -1,0 +1,247 @@
+// Factorisation of one 64x64 diagonal tile (Cholesky + inverse of the factor), shared by the
+// stand-alone diag kernel (chol.hip) and the trailing-update kernels that fuse it into the
+// workgroup that produces the tile (chol.hip, chol32.hip).
+//
+// One wave, no barriers, blocked by 16: per 16-column block the 16x16 diagonal block is factored
+// with lane r holding row r in registers (pivot by v_readlane, column broadcast through LDS,
+// 1/sqrt by v_rsq_f64 + two Newton steps) and inverted (lane c substitutes column c); the
+// 16-wide panel solve, the rank-16 trailing update and the assembly of the full inverse
+// X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb are 16x16x16 f64-MFMA products on LDS operands. The
+// inverse is kept transposed in the unused upper triangle of T (X_ab, a > b, in block (b, a); the
+// strictly lower part of X_aa in the upper part of diagonal block (a, a); its diagonal in xdg), so
+// the whole working set is 36 KB. Arithmetic is fp64 whatever the storage type of the tile.
+#pragma once
+#include "apm_internal.h"
+
+#define DP 65  // LDS pitch (doubles) of the diag kernel's tile
+
+// Broadcast lane l's value of a wave-uniform-indexed register (v_readlane x2).
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// 16x16x16 products on LDS operands with one v_mfma_f64_16x16x4_f64 chain (4 steps):
+//   NT: acc[r][c] += sum_k A[r][k] * B[c][k]      NN: acc[r][c] += sum_k A[r][k] * B[k][c]
+template <bool NEG>
+__device__ __forceinline__ void mm16_nt(d4_t& acc, const double* a, int lda, const double* b,
+                                        int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double av = a[r16 * lda + 4 * t + kq];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -av : av, b[r16 * ldb + 4 * t + kq], acc,
+                                                   0, 0, 0);
+    }
+}
+__device__ __forceinline__ void mm16_nn(d4_t& acc, const double* a, int lda, const double* b,
+                                        int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
+}
+__device__ __forceinline__ void st16(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[((lane >> 4) + 4 * q) * ld + (lane & 15)] = sgn * acc[q];
+}
+__device__ __forceinline__ void st16t(const d4_t& acc, double* dst, int ld, int lane, double sgn) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[(lane & 15) * ld + (lane >> 4) + 4 * q] = sgn * acc[q];
+}
+// Products with a diagonal block X of the inverse held as (strict lower part transposed at Td,
+// diagonal in xd): X[r][c] = c < r ? Td[c][r] : (c == r ? xd[r] : 0).
+__device__ __forceinline__ double xblk(const double* Td, const double* xd, int r, int c) {
+    return (c < r) ? Td[c * DP + r] : ((c == r) ? xd[r] : 0.0);
+}
+//   acc += A * X^T
+__device__ __forceinline__ void mm16_nt_xb(d4_t& acc, const double* a, int lda, const double* Td,
+                                           const double* xd, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   xblk(Td, xd, r16, 4 * t + kq), acc, 0, 0, 0);
+}
+//   acc += A * X
+__device__ __forceinline__ void mm16_nn_xb(d4_t& acc, const double* a, int lda, const double* Td,
+                                           const double* xd, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[r16 * lda + 4 * t + kq],
+                                                   xblk(Td, xd, 4 * t + kq, r16), acc, 0, 0, 0);
+}
+//   acc += X * B
+__device__ __forceinline__ void mm16_nn_xa(d4_t& acc, const double* Td, const double* xd,
+                                           const double* b, int ldb, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xblk(Td, xd, r16, 4 * t + kq),
+                                                   b[(4 * t + kq) * ldb + r16], acc, 0, 0, 0);
+}
+__device__ __forceinline__ void ld16(d4_t& acc, const double* src, int ld, int lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = src[((lane >> 4) + 4 * q) * ld + (lane & 15)];
+}
+
+// 64x64 Cholesky + inverse of the lower factor by ONE wave (no barriers), blocked by 16:
+// per 16-column block the 16x16 diagonal block is factored with lane r holding row r in
+// registers (pivot by v_readlane, column broadcast through LDS, 1/sqrt by v_rsq_f64 + two Newton
+// steps) and inverted (lane c substitutes column c); the 16-wide panel solve, the rank-16
+// trailing update and the assembly of the full inverse X_ab = -X_aa sum_{k=b}^{a-1} L_ak X_kb are
+// 16x16x16 f64-MFMA products on LDS operands. The inverse is kept transposed in the unused upper
+// triangle of T (X_ab, a > b, in block (b, a); the strictly lower part of X_aa in the upper part of
+// diagonal block (a, a); its diagonal in xdg): 36 KB of LDS, so that the kernel fits next to three
+// padded update workgroups on a CU (lookahead, capi.cpp).
+// Tile storage is fp64 (MatB) or fp32 (MatF, the mixed-precision Newton factorisation).
+__device__ __forceinline__ d2_t ld2(const double* p) { return *reinterpret_cast<const d2_t*>(p); }
+__device__ __forceinline__ d2_t ld2(const float* p) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    return d2_t{(double)v.x, (double)v.y};
+}
+
+struct DiagSmem {
+    double T[64 * DP];
+    double xdg[64];
+    double Tmp[16 * 17];
+    double colb[16];
+    double dg[64];
+    double yv[16];
+};
+
+// Wave-level (lane = 0..63): S.T holds the tile (pitch DP); writes L (lower, zeros above) to At,
+// inv(L) to D (row-major 64x64) and sum(log diag L) to *ldet_out. A non-positive pivot sets
+// *status = fail_code and returns early (nothing written).
+template <class TS>
+__device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet_out, int* status,
+                            int fail_code, int lane) {
+    double* T = S.T;
+    double* xdg = S.xdg;
+    double* Tmp = S.Tmp;
+    double* colb = S.colb;
+    double* dg = S.dg;
+    double* yv = S.yv;
+#pragma unroll 1
+    for (int kb = 0; kb < 4; ++kb) {
+        const int o = kb * 16;
+        // (a) factor the 16x16 diagonal block in registers: lane (g, c) = (lane >> 4, lane & 15)
+        // holds rows 4g..4g+3 of column c. Per pivot j: v_readlane of the pivot, 1/sqrt by
+        // v_rsq_f64 + two Newton steps, column j scaled by its owners (c == j) and published in
+        // LDS (colb), row values L[i][j] broadcast inside each 16-lane row group by __shfl.
+        const int c = lane & 15, g = lane >> 4;
+        double a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = T[(o + 4 * g + u) * DP + o + c];
+        bool bad = false;
+#pragma unroll 1
+        for (int j = 0; j < 16; ++j) {  // not unrolled: registers picked by selects (pressure)
+            const int ju = j & 3;
+            const double aj = ju == 0 ? a[0] : (ju == 1 ? a[1] : (ju == 2 ? a[2] : a[3]));
+            const double p = rdlane(aj, ((j >> 2) << 4) | j);
+            bad |= !(p > 0.0);
+            double y = __builtin_amdgcn_rsq(p);
+            y = y * (1.5 - 0.5 * p * y * y);
+            y = y * (1.5 - 0.5 * p * y * y);
+            if (lane == 0) {
+                yv[j] = y;
+                dg[o + j] = p * y;
+            }
+            if (c == j) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = 4 * g + u;
+                    a[u] = (i > j) ? a[u] * y : ((i == j) ? p * y : a[u]);
+                    colb[i] = a[u];
+                }
+            }
+            double lij[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) lij[u] = __shfl(a[u], (lane & 48) | j);
+            const double lcj = colb[c];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = 4 * g + u;
+                if (c > j && c <= i) a[u] -= lij[u] * lcj;
+            }
+        }
+        if (bad) {  // wave-uniform
+            if (lane == 0) *status = fail_code;
+            return;
+        }
+        // inverse X of the 16x16 factor (L X = I) for all 16 columns at once, right-looking
+        // substitution: lane (g, c) holds rows 4g..4g+3 of column c of X
+        double sx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sx[u] = (4 * g + u == c) ? 1.0 : 0.0;
+#pragma unroll 1
+        for (int r = 0; r < 16; ++r) {
+            const int ru = r & 3;
+            const double cur =
+                (ru == 0 ? sx[0] : (ru == 1 ? sx[1] : (ru == 2 ? sx[2] : sx[3]))) * yv[r];
+            const double xr = __shfl(cur, ((r >> 2) << 4) | c);  // X[r][c] (zero for c > r)
+            if (g == (r >> 2)) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (u == ru) sx[u] = cur;
+            }
+            double lir[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) lir[u] = __shfl(a[u], (lane & 48) | r);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (4 * g + u > r) sx[u] -= lir[u] * xr;
+        }
+        // L (lower incl. diagonal) back to T; X transposed into the upper part, diagonal to xdg
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = 4 * g + u;
+            if (c <= i) T[(o + i) * DP + o + c] = a[u];
+            if (i > c) T[(o + c) * DP + o + i] = sx[u];
+            if (i == c) xdg[o + c] = sx[u];
+        }
+        if (kb == 3) break;
+        // (b) panel: T[ib][kb] = T[ib][kb] * inv(L_kb,kb)^T for the blocks below
+        for (int ib = kb + 1; ib < 4; ++ib) {
+            d4_t acc = {0.0, 0.0, 0.0, 0.0};
+            mm16_nt_xb(acc, &T[(16 * ib) * DP + o], DP, &T[o * DP + o], &xdg[o], lane);
+            st16(acc, &T[(16 * ib) * DP + o], DP, lane, 1.0);
+        }
+        // (c) rank-16 trailing update of the lower blocks
+        for (int ib = kb + 1; ib < 4; ++ib)
+            for (int jb = kb + 1; jb <= ib; ++jb) {
+                d4_t acc;
+                ld16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane);
+                mm16_nt<true>(acc, &T[(16 * ib) * DP + o], DP, &T[(16 * jb) * DP + o], DP, lane);
+                st16(acc, &T[(16 * ib) * DP + 16 * jb], DP, lane, 1.0);
+            }
+    }
+    // off-diagonal blocks of the inverse, block row by block row
+#pragma unroll 1
+    for (int a = 1; a < 4; ++a)
+#pragma unroll 1
+        for (int bb = 0; bb < a; ++bb) {
+            d4_t acc = {0.0, 0.0, 0.0, 0.0};
+            mm16_nn_xb(acc, &T[(16 * a) * DP + 16 * bb], DP, &T[(16 * bb) * DP + 16 * bb],
+                       &xdg[16 * bb], lane);
+            for (int kk = bb + 1; kk < a; ++kk)  // X_kk,bb is stored transposed at T block (bb, kk)
+                mm16_nt<false>(acc, &T[(16 * a) * DP + 16 * kk], DP, &T[(16 * bb) * DP + 16 * kk],
+                               DP, lane);
+            st16(acc, Tmp, 17, lane, 1.0);
+            d4_t acc2 = {0.0, 0.0, 0.0, 0.0};
+            mm16_nn_xa(acc2, &T[(16 * a) * DP + 16 * a], &xdg[16 * a], Tmp, 17, lane);
+            st16t(acc2, &T[(16 * bb) * DP + 16 * a], DP, lane, -1.0);
+        }
+#pragma unroll 4
+    for (int q = 0; q < 64; ++q) {
+        asm volatile("" ::: "memory");  // bounded batches of LDS reads (register pressure)
+        At[(int64_t)q * ld + lane] = (TS)((lane <= q) ? T[q * DP + lane] : 0.0);
+        D[q * 64 + lane] = (TS)((lane < q) ? T[lane * DP + q] : ((lane == q) ? xdg[q] : 0.0));
+    }
+    const double l = wave_sum_d(log(dg[lane]));
+    if (lane == 0) *ldet_out = l;
+}

@@ -189,3 +189,61 @@ def test_estimators_multi_panel_vs_oracle(nat, n, d, s, kind):
     out, st, nops = ctx.theta_eval(nat.EST_LAPLACE, theta[None])
     assert abs(out[0] - lml) < 1e-7 * max(1., abs(lml)) and nops[0] == lops
     ctx.close()
+
+
+def _mixed_case(n=700, d=5, s=32):
+    from gpdemo import utils
+    X, y = utils.synthetic_gp_data(n, d, 4242, 'ard')
+    rng = np.random.RandomState(7)
+    base = 0.5 * np.log(d)
+    thetas = np.array([np.r_[0.0, np.full(d, base)],
+                       np.r_[2.0, rng.normal(scale=0.3, size=d) + base - 0.5],
+                       np.r_[4.0, rng.normal(scale=0.3, size=d) + base + 0.5]])
+    ns = rng.normal(size=(n, s))
+    return X, y, thetas, ns
+
+
+def _run_is(nat, X, y, thetas, ns, monkeypatch, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    B = len(thetas)
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, ns.shape[1], max_batch=B, n_slots=B, n_ubufs=1)
+    for k in env:
+        monkeypatch.delenv(k)
+    ctx.u_upload(0, ns)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, thetas, ubufs=[0] * B, slots=list(range(B)))
+    fs = [ctx.slot_read(b)[1] for b in range(B)]
+    ctx.close()
+    return out, st, nops, fs
+
+
+def test_mixed_newton_matches_fp64(nat, monkeypatch):
+    """The fp32 factorisation of B + one fp64 refinement step (chol32.hip) reproduces the fp64
+    Newton mode (1e-9 relative here; 1e-12 typical) and hence the estimate, for sigma = e^0..e^4."""
+    X, y, thetas, ns = _mixed_case()
+    o64, s64, n64, f64 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=0)
+    o32, s32, n32, f32 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=1)
+    assert (s64 == 0).all() and (s32 == 0).all()
+    np.testing.assert_array_equal(n32, n64)
+    for b in range(len(thetas)):
+        np.testing.assert_allclose(f32[b], f64[b], rtol=1e-9, atol=1e-9 * np.abs(f64[b]).max())
+        assert abs(o32[b] - o64[b]) <= 1e-6 * max(1.0, abs(o64[b])), (b, o32[b], o64[b])
+
+
+@pytest.mark.parametrize('tol', [0.0, 1e-7])
+def test_mixed_newton_fp64_fallback(nat, monkeypatch, tol):
+    """Chains whose refined fp32 solve fails the acceptance test are rerun in fp64 from f = 0
+    while the others keep their mixed-precision modes: tol = 0 sends every chain (results then
+    bit-identical to the fp64 path), tol = 1e-7 typically some."""
+    X, y, thetas, ns = _mixed_case()
+    o64, s64, n64, f64 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=0)
+    o32, s32, n32, f32 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=1,
+                                 APM_REFINE_TOL=tol)
+    assert (s32 == 0).all()
+    np.testing.assert_array_equal(n32, n64)
+    for b in range(len(thetas)):
+        if tol == 0.0:
+            np.testing.assert_array_equal(f32[b], f64[b])
+            assert o32[b] == o64[b]
+        else:
+            np.testing.assert_allclose(f32[b], f64[b], rtol=1e-9, atol=1e-9 * np.abs(f64[b]).max())

@@ -59,21 +59,6 @@ int main(int argc, char** argv) {
         const double fl = flops_of(t, c.kc) * chains * reps;
         printf("KS=%d %-22s tiles %6zu x %d chains: %8.3f ms/launch  %6.2f TFLOP/s\n", UPD_KS, c.name,
                t.size(), chains, ms / reps, fl / (ms * 1e-3) / 1e12);
-        if (c.kc > 1) {
-            std::vector<unsigned> tb = build_update_tiles_big(c.i0, R, c.j0, c.jend);
-            unsigned* dtb;
-            hipMalloc(&dtb, 4 * tb.size());
-            hipMemcpy(dtb, tb.data(), 4 * tb.size(), hipMemcpyHostToDevice);
-            launch_chol_update_big(M, c.k0, c.kc, dtb, (int)tb.size(), R, c.jend, lv, chains, 0);
-            hipEventRecord(e0);
-            for (int w = 0; w < reps; ++w)
-                launch_chol_update_big(M, c.k0, c.kc, dtb, (int)tb.size(), R, c.jend, lv, chains, 0);
-            hipEventRecord(e1);
-            hipEventSynchronize(e1);
-            hipEventElapsedTime(&ms, e0, e1);
-            printf("      big128 %-22s        %8.3f ms/launch  %6.2f TFLOP/s\n", c.name, ms / reps,
-                   fl / (ms * 1e-3) / 1e12);
-        }
     }
     return 0;
 }
