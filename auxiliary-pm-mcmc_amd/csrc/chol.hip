@@ -171,7 +171,7 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 }
 
 // ------------------------------------------------------------------------------- diagonal tile
-// Stand-alone diag step (one wave per chain): tile (k, k) -> LDS, diag_factor (diag.h). Used for
+// Stand-alone diag step (one wave per chain): tile (k, k) -> LDS, diag_compute + diag_store (diag.h). Used for
 // the first column of every factorisation; every later diagonal tile is factored inside the
 // update launch that produces it (k_chol_update below, fuse_diag).
 template <class Mat, class TS>
@@ -199,8 +199,12 @@ __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_
             S.T[q * DP + 2 * (lane & 31) + 1] = v[h].y;
         }
     }
-    diag_factor<TS>(S, At, A.ld, Dinv + b * dstride + (int64_t)k * 4096, ldet + b * lstride + k,
-                    live.status + b, fail_code, lane);
+    if (!diag_compute<true>(S, lane)) {
+        if (lane == 0) live.status[b] = fail_code;
+        return;
+    }
+    diag_store<TS>(S, At, A.ld, Dinv + b * dstride + (int64_t)k * 4096, ldet + b * lstride + k,
+                   lane, 64);
 }
 
 void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet, int64_t lstride,
@@ -274,7 +278,8 @@ __device__ __forceinline__ long xcd_remap(long L, long total) {
 
 // Fused diag (fd.enabled): tiles[0] must be the diagonal tile (d, d) the next column step
 // factors. Workgroups 0 .. nchains-1 (dispatched first) update chain b's tile (d, d), keep it in
-// LDS and factor it with wave 0 (diag_factor), so its latency hides under the rest of the launch;
+// LDS and factor it with wave 0 (diag_compute; all four waves store it, diag_store), so its
+// latency hides under the rest of the launch;
 // the other workgroups take the remaining (ntiles - 1) tiles of every chain.
 __global__ __launch_bounds__(256, UPD_WPE) void k_chol_update(MatB A, int k0, int kc,
                                                               const unsigned* __restrict__ tiles,
@@ -333,9 +338,17 @@ __global__ __launch_bounds__(256, UPD_WPE) void k_chol_update(MatB A, int k0, in
                 sm.d.T[(32 * wr + 16 * bi + F64_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
                        (lane & 15)] = acc[bi][bj][r];
     __syncthreads();
-    if (wv != 0) return;
-    diag_factor<double>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
-                        fd.ldet + b * fd.lstride + i, live.status + b, fd.fail_code, lane);
+    if (wv == 0) {  // rolled pivot loops: the unrolled (DPP) form would cost this kernel a wave
+        const bool ok = diag_compute<false>(sm.d, lane);
+        if (lane == 0) sm.d.ok = ok;
+    }
+    __syncthreads();
+    if (!sm.d.ok) {
+        if (threadIdx.x == 0) live.status[b] = fd.fail_code;
+        return;
+    }
+    diag_store<double>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
+                       fd.ldet + b * fd.lstride + i, threadIdx.x, 256);
 }
 
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,

@@ -175,7 +175,7 @@ __device__ __forceinline__ long xcd_remap32(long L, long total) {
 }
 
 // fd.enabled: workgroups 0 .. nchains-1 update the diagonal tile tiles[0] = (d, d) of chain b and
-// factor it in place (diag_factor, fp64 arithmetic, fp32 storage) - see k_chol_update (chol.hip).
+// factor it in place (diag_compute + diag_store, fp64 arithmetic, fp32 storage) - see k_chol_update (chol.hip).
 __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
                                                        const unsigned* __restrict__ tiles,
                                                        int ntiles, int nchains, Live live,
@@ -222,9 +222,17 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
                 sm.d.T[(32 * wr + 16 * bi + F32_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
                        (lane & 15)] = (double)acc[bi][bj][r];
     __syncthreads();
-    if (wv != 0) return;
-    diag_factor<float>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
-                       fd.ldet + b * fd.lstride + i, live.status + b, fd.fail_code, lane);
+    if (wv == 0) {
+        const bool ok = diag_compute<true>(sm.d, lane);
+        if (lane == 0) sm.d.ok = ok;
+    }
+    __syncthreads();
+    if (!sm.d.ok) {
+        if (threadIdx.x == 0) live.status[b] = fd.fail_code;
+        return;
+    }
+    diag_store<float>(sm.d, Aij, A.ld, fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
+                      fd.ldet + b * fd.lstride + i, threadIdx.x, 256);
 }
 
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,

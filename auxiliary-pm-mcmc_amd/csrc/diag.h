@@ -11,7 +11,12 @@
 // strictly lower part of X_aa in the upper part of diagonal block (a, a); its diagonal in xdg), so
 // the whole working set is 36 KB. Arithmetic is fp64 whatever the storage type of the tile.
 #pragma once
+#include <type_traits>
 #include "apm_internal.h"
+
+#ifndef DIAG_SKIP  // development bisection of the phase costs (tools/diag_test.cpp): bit mask
+#define DIAG_SKIP 0
+#endif
 
 #define DP 65  // LDS pitch (doubles) of the diag kernel's tile
 
@@ -21,6 +26,24 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u & 0xffffffffull), l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Broadcast lane j of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+).
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u & 0xffffffffull), 0x150 + J,
+                                               0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x150 + J, 0xf, 0xf,
+                                               false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int J, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (J < N) {
+        f(std::integral_constant<int, J>{});
+        static_for<J + 1, N>(f);
+    }
 }
 
 // 16x16x16 products on LDS operands with one v_mfma_f64_16x16x4_f64 chain (4 steps):
@@ -107,6 +130,7 @@ __device__ __forceinline__ d2_t ld2(const float* p) {
 
 struct DiagSmem {
     double T[64 * DP];
+    int ok;  // fused path: the factorisation succeeded (broadcast to the storing waves)
     double xdg[64];
     double Tmp[16 * 17];
     double colb[16];
@@ -114,12 +138,12 @@ struct DiagSmem {
     double yv[16];
 };
 
-// Wave-level (lane = 0..63): S.T holds the tile (pitch DP); writes L (lower, zeros above) to At,
-// inv(L) to D (row-major 64x64) and sum(log diag L) to *ldet_out. A non-positive pivot sets
-// *status = fail_code and returns early (nothing written).
-template <class TS>
-__device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet_out, int* status,
-                            int fail_code, int lane) {
+// Wave-level (lane = 0..63): factors S.T in place (L lower, inv(L) in the upper part + xdg,
+// diagonal of L in dg); returns false on a non-positive pivot (wave-uniform). UNROLLED: pivot and
+// inverse steps fully unrolled with DPP row broadcasts (fastest); the rolled form (select +
+// __shfl) needs ~10 fewer VGPRs where a kernel is at its occupancy edge.
+template <bool UNROLLED = true>
+__device__ bool diag_compute(DiagSmem& S, int lane) {
     double* T = S.T;
     double* xdg = S.xdg;
     double* Tmp = S.Tmp;
@@ -138,11 +162,44 @@ __device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet
 #pragma unroll
         for (int u = 0; u < 4; ++u) a[u] = T[(o + 4 * g + u) * DP + o + c];
         bool bad = false;
+        if constexpr (!UNROLLED) {
 #pragma unroll 1
-        for (int j = 0; j < 16; ++j) {  // not unrolled: registers picked by selects (pressure)
-            const int ju = j & 3;
-            const double aj = ju == 0 ? a[0] : (ju == 1 ? a[1] : (ju == 2 ? a[2] : a[3]));
-            const double p = rdlane(aj, ((j >> 2) << 4) | j);
+            for (int j = 0; j < ((DIAG_SKIP & 1) ? 0 : 16); ++j) {
+                const int ju = j & 3;
+                const double aj = ju == 0 ? a[0] : (ju == 1 ? a[1] : (ju == 2 ? a[2] : a[3]));
+                const double p = rdlane(aj, ((j >> 2) << 4) | j);
+                bad |= !(p > 0.0);
+                double y = __builtin_amdgcn_rsq(p);
+                y = y * (1.5 - 0.5 * p * y * y);
+                y = y * (1.5 - 0.5 * p * y * y);
+                if (lane == 0) {
+                    yv[j] = y;
+                    dg[o + j] = p * y;
+                }
+                if (c == j) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = 4 * g + u;
+                        a[u] = (i > j) ? a[u] * y : ((i == j) ? p * y : a[u]);
+                        colb[i] = a[u];
+                    }
+                }
+                double lij[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) lij[u] = __shfl(a[u], (lane & 48) | j);
+                const double lcj = colb[c];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = 4 * g + u;
+                    if (c > j && c <= i) a[u] -= lij[u] * lcj;
+                }
+            }
+        } else
+        static_for<0, ((DIAG_SKIP & 1) ? 0 : 16)>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            int js = j;  // opaque copy: the lane masks of a step are formed in that step
+            asm volatile("" : "+s"(js));
+            const double p = rdlane(a[j & 3], ((j >> 2) << 4) | j);
             bad |= !(p > 0.0);
             double y = __builtin_amdgcn_rsq(p);
             y = y * (1.5 - 0.5 * p * y * y);
@@ -151,51 +208,61 @@ __device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet
                 yv[j] = y;
                 dg[o + j] = p * y;
             }
-            if (c == j) {
+            if (c == js) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = 4 * g + u;
-                    a[u] = (i > j) ? a[u] * y : ((i == j) ? p * y : a[u]);
+                    a[u] = (i > js) ? a[u] * y : ((i == js) ? p * y : a[u]);
                     colb[i] = a[u];
                 }
             }
-            double lij[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) lij[u] = __shfl(a[u], (lane & 48) | j);
             const double lcj = colb[c];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int i = 4 * g + u;
-                if (c > j && c <= i) a[u] -= lij[u] * lcj;
+                const double lij = row_bcast<j>(a[u]);  // L[i][j]: lane j of this row group
+                if (c > js && c <= i) a[u] -= lij * lcj;
             }
-        }
-        if (bad) {  // wave-uniform
-            if (lane == 0) *status = fail_code;
-            return;
-        }
+        });
+        if (bad) return false;  // wave-uniform
         // inverse X of the 16x16 factor (L X = I) for all 16 columns at once, right-looking
         // substitution: lane (g, c) holds rows 4g..4g+3 of column c of X
         double sx[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) sx[u] = (4 * g + u == c) ? 1.0 : 0.0;
+        if constexpr (!UNROLLED) {
 #pragma unroll 1
-        for (int r = 0; r < 16; ++r) {
-            const int ru = r & 3;
-            const double cur =
-                (ru == 0 ? sx[0] : (ru == 1 ? sx[1] : (ru == 2 ? sx[2] : sx[3]))) * yv[r];
-            const double xr = __shfl(cur, ((r >> 2) << 4) | c);  // X[r][c] (zero for c > r)
-            if (g == (r >> 2)) {
+            for (int r = 0; r < ((DIAG_SKIP & 2) ? 0 : 16); ++r) {
+                const int ru = r & 3;
+                const double cur =
+                    (ru == 0 ? sx[0] : (ru == 1 ? sx[1] : (ru == 2 ? sx[2] : sx[3]))) * yv[r];
+                const double xr = __shfl(cur, ((r >> 2) << 4) | c);
+                if (g == (r >> 2)) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (u == ru) sx[u] = cur;
+                }
+                double lir[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) lir[u] = __shfl(a[u], (lane & 48) | r);
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (u == ru) sx[u] = cur;
+                    if (4 * g + u > r) sx[u] -= lir[u] * xr;
             }
-            double lir[4];
+        } else
+        static_for<0, ((DIAG_SKIP & 2) ? 0 : 16)>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            int rs = r;  // opaque copy (see the pivot loop)
+            asm volatile("" : "+s"(rs));
+            const double cur = sx[r & 3] * yv[r];
+            const double xr = __shfl(cur, ((r >> 2) << 4) | c);  // X[r][c] (zero for c > r)
+            if (g == (rs >> 2)) sx[r & 3] = cur;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) lir[u] = __shfl(a[u], (lane & 48) | r);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (4 * g + u > r) sx[u] -= lir[u] * xr;
-        }
+            for (int u = 0; u < 4; ++u) {
+                const double lir = row_bcast<r>(a[u]);  // L[4g+u][r]
+                if (4 * g + u > rs) sx[u] -= lir * xr;
+            }
+        });
         // L (lower incl. diagonal) back to T; X transposed into the upper part, diagonal to xdg
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -204,7 +271,7 @@ __device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet
             if (i > c) T[(o + c) * DP + o + i] = sx[u];
             if (i == c) xdg[o + c] = sx[u];
         }
-        if (kb == 3) break;
+        if (kb == 3 || (DIAG_SKIP & 4)) continue;
         // (b) panel: T[ib][kb] = T[ib][kb] * inv(L_kb,kb)^T for the blocks below
         for (int ib = kb + 1; ib < 4; ++ib) {
             d4_t acc = {0.0, 0.0, 0.0, 0.0};
@@ -222,7 +289,7 @@ __device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet
     }
     // off-diagonal blocks of the inverse, block row by block row
 #pragma unroll 1
-    for (int a = 1; a < 4; ++a)
+    for (int a = 1; a < ((DIAG_SKIP & 8) ? 0 : 4); ++a)
 #pragma unroll 1
         for (int bb = 0; bb < a; ++bb) {
             d4_t acc = {0.0, 0.0, 0.0, 0.0};
@@ -236,12 +303,34 @@ __device__ void diag_factor(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet
             mm16_nn_xa(acc2, &T[(16 * a) * DP + 16 * a], &xdg[16 * a], Tmp, 17, lane);
             st16t(acc2, &T[(16 * bb) * DP + 16 * a], DP, lane, -1.0);
         }
-#pragma unroll 4
-    for (int q = 0; q < 64; ++q) {
-        asm volatile("" ::: "memory");  // bounded batches of LDS reads (register pressure)
-        At[(int64_t)q * ld + lane] = (TS)((lane <= q) ? T[q * DP + lane] : 0.0);
-        D[q * 64 + lane] = (TS)((lane < q) ? T[lane * DP + q] : ((lane == q) ? xdg[q] : 0.0));
-    }
-    const double l = wave_sum_d(log(dg[lane]));
-    if (lane == 0) *ldet_out = l;
+    return true;
 }
+
+// Stores of a factored tile by `nthr` threads (64: one wave; 256: the fused update's workgroup):
+// L (zeros above the diagonal) to At, inv(L) row-major to D (16-byte stores), sum(log diag L)
+// to *ldet_out (wave 0).
+template <class TS>
+__device__ void diag_store(DiagSmem& S, TS* At, int64_t ld, TS* D, double* ldet_out, int tid,
+                           int nthr) {
+    const double* T = S.T;
+    const int p2 = 2 * (tid & 31);  // column pair
+    for (int q = tid >> 5; q < ((DIAG_SKIP & 16) ? 0 : 64); q += nthr >> 5) {
+        asm volatile("" ::: "memory");  // bounded batches of LDS reads (register pressure)
+        const double l0 = (p2 <= q) ? T[q * DP + p2] : 0.0;
+        const double l1 = (p2 + 1 <= q) ? T[q * DP + p2 + 1] : 0.0;
+        const double x0 = (p2 < q) ? T[p2 * DP + q] : ((p2 == q) ? S.xdg[q] : 0.0);
+        const double x1 = (p2 + 1 < q) ? T[(p2 + 1) * DP + q] : ((p2 + 1 == q) ? S.xdg[q] : 0.0);
+        if constexpr (sizeof(TS) == 8) {
+            *reinterpret_cast<d2_t*>(At + (int64_t)q * ld + p2) = d2_t{l0, l1};
+            *reinterpret_cast<d2_t*>(D + q * 64 + p2) = d2_t{x0, x1};
+        } else {
+            *reinterpret_cast<float2*>(At + (int64_t)q * ld + p2) = float2{(float)l0, (float)l1};
+            *reinterpret_cast<float2*>(D + q * 64 + p2) = float2{(float)x0, (float)x1};
+        }
+    }
+    if (tid < 64) {
+        const double l = wave_sum_d(log(S.dg[tid]));
+        if (tid == 0) *ldet_out = l;
+    }
+}
+
