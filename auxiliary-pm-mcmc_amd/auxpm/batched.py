@@ -1,11 +1,20 @@
 # -*- coding: utf-8 -*-
-"""Many independent APM chains advanced in lockstep on one MI355X.
+"""Many independent APM chains advanced together on one MI355X.
 
 ``BatchedAPMEllSSPlusRandDirSliceSampler`` runs ``n_chains`` copies of the reference's
 ``APMEllSSPlusRandDirSliceSampler`` transition (elliptical slice sampling on the auxiliary
 draws u, random-direction linear slice sampling on theta; reference samplers.py:1007-1089 with
-mcmc_updates.py:311-400, :403-519) as masked lockstep rounds: every shrink iteration of every
-still-undecided chain is one batched estimator call, so the device always sees a batch.
+mcmc_updates.py:311-400, :403-519). Two schedules share the per-chain code:
+
+* ``step()``: lockstep — every chain does one whole transition; each shrink iteration of every
+  still-undecided chain is one batched estimator call (late rounds carry few chains).
+* ``run(...)`` / ``run_async(...)``: asynchronous — each chain is a small state machine and every
+  round issues ONE batched theta-call for all chains whose random-direction slice step needs an
+  evaluation, after first completing (with cheap batched u-calls) the elliptical slice update of
+  every chain that has just finished a transition. Chains never wait for each other, so every
+  theta-call carries the whole batch. Each chain's sequence of estimator calls and host-RNG draws
+  is unchanged, so its trajectory is identical to the lockstep (and, up to the device u, to the
+  reference's sequential) run; tests/test_gpu_batched.py checks async == lockstep bitwise.
 
 Per chain the control flow, the cache protocol and the host-RNG draw order are those of the
 reference (one ``numpy.random.RandomState`` per chain for the slice heights, angles, offsets and
@@ -67,6 +76,18 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.n_theta_calls = 0
         self.n_u_calls = 0
         self.n_cubic_ops = np.zeros(C, dtype=np.int64)
+        # asynchronous random-direction slice state (one pending theta per chain)
+        self._rd_d = np.zeros((C, self.P))
+        self._rd_logy = np.zeros(C)
+        self._rd_lo = np.zeros(C)
+        self._rd_hi = np.zeros(C)
+        self._rd_x = np.zeros(C)
+        self._rd_mode = np.zeros(C, dtype=np.int64)  # 0: step down, 1: step up, 2: shrink
+        self._rd_s = np.zeros(C, dtype=np.int64)
+        self._rd_down = np.zeros(C)
+        self._rd_up = np.zeros(C)
+        self._rd_it = np.zeros(C, dtype=np.int64)
+        self._rd_pend = np.zeros((C, self.P))
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
@@ -106,9 +127,11 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         return self.theta.copy()
 
     # ------------------------------------------------------------------ updates
-    def _ess_u(self):
-        """Elliptical slice update of every live chain's u (mcmc_updates.py:372-400)."""
-        live = np.flatnonzero(~self.failed)
+    def _ess_u(self, chains=None):
+        """Elliptical slice update of the u of every live chain (or of the given chains),
+        mcmc_updates.py:372-400; each shrink round is one batched u-call."""
+        live = np.flatnonzero(~self.failed) if chains is None else \
+            np.asarray(chains, dtype=np.int64)[~self.failed[chains]]
         if live.size == 0:
             return
         self._normals(live, self.ub_nu)
@@ -224,14 +247,131 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
                 act = grow[s[grow] < budget[grow]]
 
     def step(self):
-        """One transition (u then theta) of every live chain; returns thetas (n_chains, P)."""
+        """One lockstep transition (u then theta) of every live chain; returns thetas
+        (n_chains, P)."""
         self._ess_u()
         self._rdss_theta()
         return self.theta.copy()
 
+    # ------------------------------------------------------------------ asynchronous schedule
+    def _rd_begin(self, c):
+        """Start chain c's random-direction slice step: the draws of mcmc_updates.py:480-490 in
+        the reference order (direction, slice height, bracket offset, step-out split)."""
+        rng = self.prngs[c]
+        dd = rng.normal(size=self.P)
+        self._rd_d[c] = dd / dd.dot(dd) ** 0.5
+        self._rd_logy[c] = np.log(rng.uniform()) + self.log_f[c]
+        self._rd_lo[c] = 0. - self.w * rng.uniform()
+        self._rd_hi[c] = self._rd_lo[c] + self.w
+        self._rd_s[c] = 0
+        self._rd_it[c] = 0
+        if self.max_steps_out > 0:
+            self._rd_down[c] = np.round(rng.uniform() * self.max_steps_out)
+            self._rd_up[c] = self.max_steps_out - self._rd_down[c]
+            self._rd_mode[c] = 0
+        else:
+            self._rd_mode[c] = 2
+        self._rd_next(c)
+
+    def _rd_next(self, c):
+        """Set chain c's next theta to evaluate (a step-out probe or a shrink proposal)."""
+        if self._rd_mode[c] == 0:
+            if self._rd_s[c] < self._rd_down[c]:
+                self._rd_pend[c] = self.theta[c] + self._rd_lo[c] * self._rd_d[c]
+                return
+            self._rd_mode[c], self._rd_s[c] = 1, 0
+        if self._rd_mode[c] == 1:
+            if self._rd_s[c] < self._rd_up[c]:
+                self._rd_pend[c] = self.theta[c] + self._rd_hi[c] * self._rd_d[c]
+                return
+            self._rd_mode[c] = 2
+        self._rd_x[c] = self._rd_lo[c] + (self._rd_hi[c] - self._rd_lo[c]) * \
+            self.prngs[c].uniform()
+        self._rd_pend[c] = self.theta[c] + self._rd_x[c] * self._rd_d[c]
+
+    def _rd_result(self, c, lf):
+        """Consume the estimate at chain c's pending theta; True when the transition is done."""
+        mode = self._rd_mode[c]
+        if mode < 2:  # step out while the bracket end is inside the slice (mcmc_updates.py:491-498)
+            if self._rd_logy[c] < lf:
+                if mode == 0:
+                    self._rd_lo[c] -= self.w
+                else:
+                    self._rd_hi[c] += self.w
+                self._rd_s[c] += 1
+            else:
+                self._rd_mode[c], self._rd_s[c] = mode + 1, 0
+            self._rd_next(c)
+            return False
+        if lf > self._rd_logy[c]:  # accept: the proposal's cache becomes current
+            self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
+            self.theta[c] = self._rd_pend[c]
+            self.log_f[c] = lf
+            return True
+        if self.failed[c]:
+            return True
+        x = self._rd_x[c]
+        if x < 0.:
+            self._rd_lo[c] = x
+        elif x > 0.:
+            self._rd_hi[c] = x
+        else:
+            warnings.warn('Slice collapsed to current value')
+            return True
+        self._rd_it[c] += 1
+        if self._rd_it[c] >= self.max_slice_iters:
+            self.failed[c] = True
+            return True
+        self._rd_next(c)
+        return False
+
+    def run_async(self, n_steps, keep_going=False):
+        """Advance every live chain by at least ``n_steps`` transitions with the asynchronous
+        schedule. keep_going=False: a chain stops after n_steps (the call ends with every chain
+        at a transition boundary); True: chains that are ahead keep working until the slowest
+        has n_steps (throughput mode; a final partial transition is discarded).
+        Returns (traces, done): per chain the list of thetas after each completed transition and
+        the number of completed transitions."""
+        C = self.n_chains
+        done = np.zeros(C, dtype=np.int64)
+        traces = [[] for _ in range(C)]
+        need_u = ~self.failed
+        in_rd = np.zeros(C, dtype=bool)
+        while True:
+            unfinished = (~self.failed) & (done < n_steps)
+            if not unfinished.any():
+                break
+            go = (~self.failed) & (unfinished if not keep_going else True)
+            ess = np.flatnonzero(need_u & go)
+            if ess.size:
+                self._ess_u(ess)
+                for c in ess:
+                    need_u[c] = False
+                    if not self.failed[c]:
+                        self._rd_begin(c)
+                        in_rd[c] = True
+            rd = np.flatnonzero(in_rd & ~self.failed)
+            if rd.size == 0:
+                break
+            lf = self._theta_eval(rd, self._rd_pend[rd], self.slot_prop[rd])
+            for q, c in enumerate(rd):
+                if self._rd_result(c, lf[q]):
+                    in_rd[c] = False
+                    if not self.failed[c]:
+                        done[c] += 1
+                        traces[c].append(self.theta[c].copy())
+                        need_u[c] = True
+        return traces, done
+
     def run(self, n_steps, theta_init=None, warmup_callback=None):
+        """(n_chains, n_steps, P) trace starting at the initial state, asynchronous schedule
+        (identical per-chain trajectories to n_steps - 1 lockstep ``step()`` calls)."""
         thetas = np.empty((self.n_chains, n_steps, self.P))
         thetas[:, 0] = self.initialise(theta_init)
-        for s in range(1, n_steps):
-            thetas[:, s] = self.step()
+        traces, done = self.run_async(n_steps - 1)
+        for c in range(self.n_chains):
+            k = int(done[c])
+            if k:
+                thetas[c, 1:1 + k] = np.array(traces[c])
+            thetas[c, 1 + k:] = self.theta[c]  # failed chains: frozen at their last state
         return thetas

@@ -42,6 +42,8 @@ def parse():
     ap.add_argument('--d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
+    ap.add_argument('--schedule', choices=('async', 'lockstep'), default='async',
+                    help='chain scheduling of the batched sampler (auxpm/batched.py)')
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=30.0,
                     help='approximate seconds of CPU work for the baseline sample')
@@ -175,25 +177,42 @@ def main():
         seed=a.seed + 7919 * dist.rank, device=dist.local_rank)
     P = smp.P
     smp.initialise()
-    for _ in range(a.warmup):
-        smp.step()
+    if a.schedule == 'async':
+        if a.warmup:
+            smp.run_async(a.warmup)  # every chain W transitions, ending on a transition boundary
+    else:
+        for _ in range(a.warmup):
+            smp.step()
     ctx = smp.ctx
     for k in (0, 1, 2, 3):
         ctx.prof_read(k, reset=True)
     ctx.prof_enable(True)
-    thetas = []
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
+    res = {}
+    if a.schedule == 'async':
+        # every chain completes >= K transitions; chains that are ahead keep working until the
+        # slowest has K (every theta-call carries the full batch); all completed transitions
+        # count, a final partial transition of a chain is discarded
+        def body():
+            res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
+        elapsed = timed_region(dist, body, 1)
+        done = res['done']
+        tr_list = [np.array(res['traces'][c][:a.steps]) for c in range(a.chains)
+                   if not smp.failed[c] and done[c] >= a.steps]
+    else:
+        thetas = []
 
-    def one_step():
-        thetas.append(smp.step())
-
-    elapsed = timed_region(dist, one_step, a.steps)
+        def one_step():
+            thetas.append(smp.step())
+        elapsed = timed_region(dist, one_step, a.steps)
+        done = np.where(smp.failed, 0, a.steps)
+        tr_list = [np.stack(thetas, 1)[c] for c in range(a.chains) if not smp.failed[c]]
     ctx.prof_enable(False)
-    live = int((~smp.failed).sum())
-    transitions = dist.sum(live * a.steps)
+    local_tr = int(done[~smp.failed].sum())
+    transitions = dist.sum(local_tr)
     value = transitions / elapsed
-    n_th = (smp.n_theta_calls - th0) / max(1, a.chains * a.steps)
-    n_u = (smp.n_u_calls - u0) / max(1, a.chains * a.steps)
+    n_th = (smp.n_theta_calls - th0) / max(1, local_tr)
+    n_u = (smp.n_u_calls - u0) / max(1, local_tr)
 
     prof = {}
     for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32')):
@@ -240,9 +259,8 @@ def main():
                                 'avg_launch_us': ums * 1e3 / ucnt,
                                 'algorithmic_flops_per_launch': uflops / ucnt}
     ess_per_sec = None
-    if a.steps >= 100:
-        tr = np.stack(thetas, 1)  # (chains, steps, P)
-        ess = sum(effective_size(tr[c]).min() for c in range(a.chains) if not smp.failed[c])
+    if a.steps >= 100:  # min over theta components of each chain's ESS over its first K steps
+        ess = sum(effective_size(t).min() for t in tr_list)
         ess_per_sec = dist.sum(ess) / elapsed
 
     cpu = None
@@ -270,6 +288,7 @@ def main():
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
                    .format(dist.world)},
         'ess_per_sec': ess_per_sec,
+        'schedule': a.schedule, 'transitions_timed': int(transitions),
         'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
         'failed_chains': int(dist.sum(int(smp.failed.sum()))),
         'roofline': roofline, 'cpu_baseline': cpu,
