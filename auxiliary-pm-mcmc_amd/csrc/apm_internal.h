@@ -58,6 +58,8 @@ std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int gl
 // z written to z[b*zstride + ...]
 void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_t dstride,
                          double* z, int64_t zstride, Live live, int nchains, hipStream_t s);
+// empty kernel k_apm_marker<id> (trace bracketing, apm_prof_marker)
+void launch_marker(int id, hipStream_t s);
 // test hook: C(64x64) = A(64x64) * B(64x64)^T through the MFMA tile path
 void launch_tile_nt_test(const double* A, const double* B, double* C, hipStream_t s);
 

@@ -1008,6 +1008,18 @@ int apm_prof_enable(apm_ctx* c, int on) {
     return APM_SUCCESS;
 }
 
+int apm_prof_marker(apm_ctx* c, int id) {
+    if (!c || id < 0 || id > 3) return fail(c, APM_E_INVALID, "apm_prof_marker: bad arguments");
+    try {
+        HIPC(hipSetDevice(c->device));
+        launch_marker(id, c->stream);
+        check_launch();
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
 int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, double* work,
                   int reset) {
     if (!c || kind < 0 || kind >= APM_PROF_NKINDS)

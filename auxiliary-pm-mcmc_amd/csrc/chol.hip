@@ -433,3 +433,16 @@ __global__ __launch_bounds__(256) void k_tile_nt_test(const double* A, const dou
 void launch_tile_nt_test(const double* A, const double* B, double* C, hipStream_t s) {
     hipLaunchKernelGGL(k_tile_nt_test, dim3(1), dim3(256), 0, s, A, B, C);
 }
+
+// ------------------------------------------------------------------------------- trace markers
+template <int ID>
+__global__ void k_apm_marker() {}
+
+void launch_marker(int id, hipStream_t s) {
+    switch (id) {
+        case 0: hipLaunchKernelGGL(k_apm_marker<0>, dim3(1), dim3(64), 0, s); break;
+        case 1: hipLaunchKernelGGL(k_apm_marker<1>, dim3(1), dim3(64), 0, s); break;
+        case 2: hipLaunchKernelGGL(k_apm_marker<2>, dim3(1), dim3(64), 0, s); break;
+        default: hipLaunchKernelGGL(k_apm_marker<3>, dim3(1), dim3(64), 0, s); break;
+    }
+}

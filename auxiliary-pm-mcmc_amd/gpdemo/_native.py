@@ -54,6 +54,7 @@ _SIGS = {
     'apm_gram': (_i, [_i, _i, _p, _i64, _i64, _i64, _p, _i64, _d, _p, _i64]),
     'apm_laplace': (_i, [_i, _p, _i64, _i64, _p, _i, _i, _d, _i64, _p, _p, _i64, _p, _p, _p]),
     'apm_prof_enable': (_i, [_p, _i]),
+    'apm_prof_marker': (_i, [_p, _i]),
     'apm_prof_read': (_i, [_p, _i, _p, _p, _p, _i]),
     'apm_selftest_tile': (_i, [_i, _p, _p, _p]),
 }
@@ -295,6 +296,9 @@ class Context(object):
     # --- profiling
     def prof_enable(self, on=True):
         _check(self.lib.apm_prof_enable(self._h, int(bool(on))), self._h)
+
+    def prof_marker(self, marker_id):
+        _check(self.lib.apm_prof_marker(self._h, int(marker_id)), self._h)
 
     def prof_read(self, kind, reset=False):
         ms = np.zeros(1)

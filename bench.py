@@ -107,6 +107,20 @@ def device_sync():
         pass
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per dispatch of `kernel` inside the timed region, from the newest committed
+    PMC pass of this bench (profiles/r*_pmc_traffic.json, written by tools/prof_window.py from
+    separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of the same command, with the
+    guide's gfx950 corrections). PMC counters cannot be read live inside this process."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1])).get('pmc_traffic', {}).get(kernel, {})
+    b = d.get('traffic_bytes_per_dispatch')
+    return b, (os.path.relpath(files[-1], REPO) if b is not None else None)
+
+
 def timed_region(dist, step_fn, steps):
     """barrier + sync, K steps, barrier + sync; returns the max over ranks of the wall time."""
     dist.barrier()
@@ -187,6 +201,7 @@ def main():
     for k in (0, 1, 2, 3):
         ctx.prof_read(k, reset=True)
     ctx.prof_enable(True)
+    ctx.prof_marker(1)  # timed-region brackets for rocprofv3 traces (tools/prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
     res = {}
     if a.schedule == 'async':
@@ -207,6 +222,7 @@ def main():
         elapsed = timed_region(dist, one_step, a.steps)
         done = np.where(smp.failed, 0, a.steps)
         tr_list = [np.stack(thetas, 1)[c] for c in range(a.chains) if not smp.failed[c]]
+    ctx.prof_marker(2)
     ctx.prof_enable(False)
     local_tr = int(done[~smp.failed].sum())
     transitions = dist.sum(local_tr)
@@ -219,23 +235,26 @@ def main():
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
 
-    def mfma_roofline(name, kernel, peak):
+    def mfma_roofline(name, kernel, peak, short):
         ms, cnt, flops = prof[name]
         if not cnt:
             return None
         avg_s = ms * 1e-3 / cnt
         achieved = (flops / cnt) / avg_s / 1e12
+        tr, src = pmc_traffic(short)
         return {'kernel': kernel, 'bound': 'mfma', 'achieved': achieved, 'peak': peak,
-                'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
+                'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': tr,
+                'traffic_unit': 'HBM bytes per launch', 'traffic_source': src,
                 'launches': cnt, 'avg_launch_us': avg_s * 1e6,
                 'algorithmic_flops_per_launch': flops / cnt,
                 'share_of_step_time': (ms * 1e-3) / elapsed}
 
     upd64 = mfma_roofline('chol_update', 'k_chol_update (f64 MFMA trailing update of the '
                           'fp64 factorisations: chol(K), SYRK + chol of I + L_K^T W L_K)',
-                          PEAK_F64_MFMA_TFLOPS)
+                          PEAK_F64_MFMA_TFLOPS, 'k_chol_update')
     upd32 = mfma_roofline('chol_update32', 'k_chol_update32 (f32 MFMA trailing update of the '
-                          'mixed-precision Newton factorisation of B)', PEAK_F32_MFMA_TFLOPS)
+                          'mixed-precision Newton factorisation of B)', PEAK_F32_MFMA_TFLOPS,
+                          'k_chol_update32')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])
@@ -246,16 +265,19 @@ def main():
     gms, gcnt, gbytes = prof['gram']
     if gcnt:
         ach = gbytes / (gms * 1e-3) / 1e12
+        tr, src = pmc_traffic('k_gram')
         extra['roofline_gram'] = {'bound': 'hbm', 'achieved': ach, 'peak': PEAK_HBM_TBS,
-                                  'unit': 'TB/s', 'frac': ach / PEAK_HBM_TBS, 'traffic': None,
+                                  'unit': 'TB/s', 'frac': ach / PEAK_HBM_TBS, 'traffic': tr,
+                                  'traffic_source': src,
                                   'launches': gcnt, 'avg_launch_us': gms * 1e3 / gcnt,
                                   'algorithmic_bytes_per_launch': gbytes / gcnt}
     ums, ucnt, uflops = prof['ugemm']
     if ucnt:
         ach = uflops / (ums * 1e-3) / 1e12
+        tr, src = pmc_traffic('k_ugemm')
         extra['roofline_lu'] = {'bound': 'mfma', 'achieved': ach, 'peak': PEAK_F32_MFMA_TFLOPS,
                                 'unit': 'TFLOP/s', 'frac': ach / PEAK_F32_MFMA_TFLOPS,
-                                'traffic': None, 'launches': ucnt,
+                                'traffic': tr, 'traffic_source': src, 'launches': ucnt,
                                 'avg_launch_us': ums * 1e3 / ucnt,
                                 'algorithmic_flops_per_launch': uflops / ucnt}
     ess_per_sec = None

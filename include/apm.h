@@ -123,6 +123,9 @@ int apm_prof_enable(apm_ctx *ctx, int on);
  * factorisation, UGEMM) those launches performed */
 int apm_prof_read(apm_ctx *ctx, int kind, double *total_ms, int64_t *launches, double *work,
                   int reset);
+/* launches the empty kernel k_apm_marker<id> (id 0..3) on the context stream: brackets a region
+ * in a rocprofv3 kernel trace (tools/prof_window.py); no reference counterpart */
+int apm_prof_marker(apm_ctx *ctx, int id);
 
 /* ---- self-test ------------------------------------------------------------------------------- */
 /* C = C + A * B^T for 64x64 row-major fp64 host matrices through the f64 MFMA tile routine that

@@ -1,0 +1,9 @@
+# Round profile of the default bench (3 timed steps): kernel trace + stats, then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE) of the same command; outputs under gpurun_out/prof_round/.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/prof_round
+CMD="python3 bench.py --steps 3 --cpu-baseline 0"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $CMD > $O.trace.json 2> $O.trace.err
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o run -- $CMD > $O.fetch.json 2> $O.fetch.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o run -- $CMD > $O.write.json 2> $O.write.err
