@@ -15,6 +15,7 @@
 // tile lists (f32 MFMA v_mfma_f32_16x16x4_f32: twice the fp64 MFMA rate, half the bytes), blocked
 // forward / backward TRSV with fp32 tiles and fp64 vectors, and the refinement vector ops.
 #include <algorithm>
+#include <vector>
 
 #include "apm_internal.h"
 #include "diag.h"

@@ -35,8 +35,8 @@ PEAK_HBM_TBS = 8.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=100, help='timed transitions per chain (ESS/s needs >= 100)')
+    ap.add_argument('--warmup', type=int, default=20, help='untimed transitions per chain (burn-in)')
     ap.add_argument('--chains', type=int, default=64, help='chains per GPU')
     ap.add_argument('--n', type=int, default=4096)
     ap.add_argument('--d', type=int, default=32)
