@@ -71,9 +71,11 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0});
-struct NewtonVecs;
-void launch_form_B32(MatB K, MatF Bf, NewtonVecs v, int np, Live live, int nchains,
-                     hipStream_t s);
+// y = K x from K's lower tiles (part: nb*nb*64 doubles per chain of partials); Bf.base != null
+// also forms the fp32 Newton matrix I + W^1/2 K W^1/2 and its right-hand-side block (x = b)
+void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,
+                 double* part, int64_t pstride, int np, MatF Bf, const double* Ws,
+                 int64_t wstride, Live live, int nchains, hipStream_t s);
 void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Live live,
                   int nchains, hipStream_t s);
 // blocked TRSV steps with fp32 tiles / inverses and fp64 vectors (r updated in place)

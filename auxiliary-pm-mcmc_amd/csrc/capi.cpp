@@ -47,6 +47,8 @@ struct apm_ctx {
     NewtonVecs v{};
     double* vecbase = nullptr;
     double* rvec = nullptr;   // 3 refinement vectors per chain (mixed-precision Newton)
+    double* sympart = nullptr;  // symmetric K x partials: nb*nb*64 per chain (launch_symv)
+    int64_t sstride = 0;
     bool mixed = true;        // APM_MIXED=0: fp64 Newton factorisation (development knob)
     int n_refine = 1;         // APM_REFINE overrides
     double refine_tol = 1e-3; // last correction / solution (max norms) accepted by the check
@@ -302,9 +304,7 @@ void newton_solve32(apm_ctx* c, int count) {
     MatF F = b32_of(c);
     float* D = dinv32_of(c);
     double *r1 = c->rvec, *r2 = c->rvec + c->max_batch * vs, *r3 = c->rvec + 2 * c->max_batch * vs;
-    launch_form_B32(c->K, F, c->v, np, lv, count, s);
-    check_launch();
-    chol_range32(c, F, 0, nb, nb + 1, nb, APM_STATUS_CHOL_B, count);
+    chol_range32(c, F, 0, nb, nb + 1, nb, APM_STATUS_CHOL_B, count);  // B32 formed with K b
     launch_row32(F, np, np, r1, vs, lv, count, s);  // y0 = L^-1 rhs (fp32)
     check_launch();
     for (int J = nb - 1; J >= 0; --J) {
@@ -314,7 +314,8 @@ void newton_solve32(apm_ctx* c, int count) {
     for (int it = 0; it < c->n_refine; ++it) {
         launch_refine(0, c->v.Ws, c->v.Kb, c->v.z, nullptr, r2, vs, np, lv, count, s);  // t
         check_launch();
-        launch_gemv(c->K, r2, vs, r3, vs, np, lv, count, s);                             // K t
+        launch_symv(c->K, r2, vs, r3, vs, c->sympart, c->sstride, np, MatF{}, nullptr, 0, lv,
+                    count, s);                                                           // K t
         check_launch();
         launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lv, count, s);       // res
         check_launch();
@@ -347,8 +348,13 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
     for (; it < c->max_iters; ++it) {
         launch_newton_prep(c->v, c->y, c->n, c->np, lv, count, c->stream);
         check_launch();
-        launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
-                    c->stream);
+        if (mixed) {  // K b and the fp32 B (+ its right-hand side) in one pass over K's lower half
+            launch_symv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->sympart, c->sstride,
+                        c->np, b32_of(c), c->v.Ws, c->v.vstride, lv, count, c->stream);
+        } else {
+            launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
+                        c->stream);
+        }
         check_launch();
         if (mixed) {
             newton_solve32(c, count);
@@ -364,8 +370,12 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
         }
         launch_newton_update(c->v, c->np, lv, count, c->stream);
         check_launch();
-        launch_gemv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->np, lv, count,
-                    c->stream);
+        if (mixed)
+            launch_symv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->sympart,
+                        c->sstride, c->np, MatF{}, nullptr, 0, lv, count, c->stream);
+        else
+            launch_gemv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->np, lv, count,
+                        c->stream);
         check_launch();
         launch_newton_check(c->v, c->n, c->np, c->tol, c->active, c->status, c->n_iter, count,
                             c->stream);
@@ -581,6 +591,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     const int64_t vs = np;
     c->vecbase = dalloc<double>(c, 8 * B * vs);
     c->rvec = dalloc<double>(c, 3 * B * vs);
+    c->sstride = (int64_t)c->nb * c->nb * 64;
+    c->sympart = dalloc<double>(c, B * c->sstride);
     c->v = NewtonVecs{c->vecbase,          c->vecbase + 1 * B * vs, c->vecbase + 2 * B * vs,
                       c->vecbase + 3 * B * vs, c->vecbase + 4 * B * vs, c->vecbase + 5 * B * vs,
                       c->vecbase + 6 * B * vs, c->vecbase + 7 * B * vs, vs};

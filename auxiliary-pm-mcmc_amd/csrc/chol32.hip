@@ -245,44 +245,7 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 }
 
 // ------------------------------------------------------------------------------- B in fp32
-// lower tiles of B32 = I + W^1/2 K W^1/2 (formed in fp64, rounded once); rows [np, np+64): the
-// right-hand side W^1/2 (K b) in row np, zeros below (forward-solved by the factorisation)
-__global__ __launch_bounds__(256) void k_form_B32(MatB K, MatF Bf, NewtonVecs v, int nb,
-                                                  Live live) {
-    const int b = blockIdx.y;
-    if (!live32(live, b)) return;
-    const int t = blockIdx.x, ntri = nb * (nb + 1) / 2;
-    const double* Kb = K.base + b * K.cstride;
-    float* Fb = Bf.base + b * Bf.cstride;
-    const double* Ws = v.Ws + b * v.vstride;
-    const int tid = threadIdx.x;
-    if (t < ntri) {
-        int ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while (ti * (ti + 1) / 2 > t) --ti;
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        const int tj = t - ti * (ti + 1) / 2;
-        for (int e = tid; e < 4096; e += 256) {
-            const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
-            const double kv = Kb[(int64_t)r * K.ld + c];
-            Fb[(int64_t)r * Bf.ld + c] = (float)((r == c ? 1.0 : 0.0) + (Ws[r] * kv) * Ws[c]);
-        }
-    } else {
-        const int tj = t - ntri;
-        const int64_t r0 = (int64_t)nb * 64;
-        const double* Kbv = v.Kb + b * v.vstride;
-        for (int e = tid; e < 4096; e += 256) {
-            const int rr = e >> 6, c = tj * 64 + (e & 63);
-            Fb[(r0 + rr) * Bf.ld + c] = (rr == 0) ? (float)(Ws[c] * Kbv[c]) : 0.0f;
-        }
-    }
-}
-
-void launch_form_B32(MatB K, MatF Bf, NewtonVecs v, int np, Live live, int nchains,
-                     hipStream_t s) {
-    const int nb = np / 64;
-    hipLaunchKernelGGL(k_form_B32, dim3(nb * (nb + 1) / 2 + nb, nchains), dim3(256), 0, s, K, Bf,
-                       v, nb, live);
-}
+// (formed by k_symv_part in the same pass as K b, below)
 
 // out[b][:] = row `row` of Bf (fp32 -> fp64)
 __global__ __launch_bounds__(256) void k_row32(MatF Bf, int64_t row, int np, double* out,
@@ -297,6 +260,97 @@ void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Li
                   int nchains, hipStream_t s) {
     hipLaunchKernelGGL(k_row32, dim3((np + 255) / 256, nchains), dim3(256), 0, s, Bf, row, np,
                        out, ostride, live);
+}
+
+// ------------------------------------------------------------------------------- K x (symmetric)
+// y = K x reading only K's lower tiles (half the bytes of a full GEMV): workgroup (ti, tj) stages
+// tile K_ij in LDS and writes the partial products K_ij x_j (row sums) to part[ti][tj] and, off
+// the diagonal, K_ij^T x_i (column sums) to part[tj][ti]; k_symv_reduce adds the nb partials of
+// every row in a fixed order (deterministic, no atomics). With `Bf` set, the same pass also
+// writes the fp32 Newton matrix tile I + W^1/2 K W^1/2 (fusing k_form_B32 into the x = b pass).
+__global__ __launch_bounds__(256) void k_symv_part(MatB K, const double* __restrict__ x,
+                                                   int64_t xstride, double* __restrict__ part,
+                                                   int64_t pstride, int nb, MatF Bf,
+                                                   const double* __restrict__ Ws, int64_t wstride,
+                                                   Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int t = blockIdx.x;
+    int ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > t) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    const int tj = t - ti * (ti + 1) / 2;
+    __shared__ double T[64][65];
+    __shared__ double xi[64], xj[64];
+    const int tid = threadIdx.x;
+    const double* Kt = K.base + b * K.cstride + (int64_t)(ti * 64) * K.ld + tj * 64;
+    const double* wb = Ws ? Ws + b * wstride : nullptr;
+    float* Fb = Bf.base ? Bf.base + b * Bf.cstride + (int64_t)(ti * 64) * Bf.ld + tj * 64 : nullptr;
+#pragma unroll 4
+    for (int e = tid; e < 2048; e += 256) {  // 16-byte loads, rows of 512 B
+        const int r = e >> 5, c2 = (e & 31) * 2;
+        const d2_t v = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld + c2);
+        T[r][c2] = v.x;
+        T[r][c2 + 1] = v.y;
+        if (Fb) {
+            const int gr = ti * 64 + r, gc = tj * 64 + c2;
+            const double wr_ = wb[gr];
+            float2 o;
+            o.x = (float)((gr == gc ? 1.0 : 0.0) + (wr_ * v.x) * wb[gc]);
+            o.y = (float)((gr == gc + 1 ? 1.0 : 0.0) + (wr_ * v.y) * wb[gc + 1]);
+            *reinterpret_cast<float2*>(Fb + (int64_t)r * Bf.ld + c2) = o;
+        }
+    }
+    const double* xb = x + b * xstride;
+    if (tid < 64) xj[tid] = xb[tj * 64 + tid];
+    else if (tid < 128) xi[tid - 64] = xb[ti * 64 + tid - 64];
+    __syncthreads();
+    double* pb = part + b * pstride;
+    if (tid < 64) {  // row sums: part[ti][tj][r]
+        double s = 0.0;
+#pragma unroll 8
+        for (int c = 0; c < 64; ++c) s = fma(T[tid][c], xj[c], s);
+        pb[((int64_t)ti * nb + tj) * 64 + tid] = s;
+    } else if (tid < 128 && ti != tj) {  // column sums: part[tj][ti][c]
+        const int c = tid - 64;
+        double s = 0.0;
+#pragma unroll 8
+        for (int r = 0; r < 64; ++r) s = fma(T[r][c], xi[r], s);
+        pb[((int64_t)tj * nb + ti) * 64 + c] = s;
+    }
+}
+
+// y[i] = sum_tj part[i/64][tj][i%64]; with Bf: also the Newton right-hand-side block of the fp32
+// matrix (row np = W^1/2 y, rows np+1 .. np+63 zero)
+__global__ __launch_bounds__(256) void k_symv_reduce(const double* __restrict__ part,
+                                                     int64_t pstride, int nb, double* y,
+                                                     int64_t ystride, MatF Bf,
+                                                     const double* __restrict__ Ws,
+                                                     int64_t wstride, Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int np = nb * 64;
+    if (i >= np) return;
+    const double* pb = part + b * pstride + (int64_t)(i >> 6) * nb * 64 + (i & 63);
+    double s = 0.0;
+    for (int tj = 0; tj < nb; ++tj) s += pb[(int64_t)tj * 64];
+    y[b * ystride + i] = s;
+    if (Bf.base) {
+        float* col = Bf.base + b * Bf.cstride + (int64_t)np * Bf.ld + i;
+        col[0] = (float)(Ws[b * wstride + i] * s);
+        for (int r = 1; r < 64; ++r) col[(int64_t)r * Bf.ld] = 0.0f;
+    }
+}
+
+void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,
+                 double* part, int64_t pstride, int np, MatF Bf, const double* Ws,
+                 int64_t wstride, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_symv_part, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, K, x,
+                       xstride, part, pstride, nb, Bf, Ws, wstride, live);
+    hipLaunchKernelGGL(k_symv_reduce, dim3((np + 255) / 256, nchains), dim3(256), 0, s, part,
+                       pstride, nb, y, ystride, Bf, Ws, wstride, live);
 }
 
 // ------------------------------------------------------------------------------- TRSV
