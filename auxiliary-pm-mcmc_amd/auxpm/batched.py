@@ -24,12 +24,13 @@ device, so trajectories are statistically — not bitwise — equivalent to a nu
 (DESIGN.md §6). The log target is estimator + log-Gamma prior (E-SS+RD-SS.ipynb:167-173), the
 tau prior applied to every ARD length-scale (gpdemo.utils.log_prior_ard).
 """
+import time
 import warnings
 
 import numpy as np
 
 from gpdemo import _native
-from gpdemo.utils import log_prior_ard
+from gpdemo.utils import log_prior_ard_batch
 
 __all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler']
 
@@ -71,11 +72,14 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.dev_ctr = np.zeros(C, dtype=np.uint64)
         self.theta = np.zeros((C, self.P))
         self.log_f = np.full(C, -np.inf)
+        self.lp_cur = np.zeros(C)  # log prior of the current theta (constant during the u-update)
         self.failed = np.zeros(C, dtype=bool)
         self.fail_status = np.zeros(C, dtype=np.int32)
         self.n_theta_calls = 0
         self.n_u_calls = 0
         self.n_cubic_ops = np.zeros(C, dtype=np.int64)
+        # wall seconds inside the device calls (the rest of a run is host-side sampler logic)
+        self.wall = {'theta_call': 0., 'u_call': 0., 'u_draw': 0.}
         # asynchronous random-direction slice state (one pending theta per chain)
         self._rd_d = np.zeros((C, self.P))
         self._rd_logy = np.zeros(C)
@@ -91,14 +95,19 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
-        return np.array([log_prior_ard(t, self.prior) for t in np.atleast_2d(thetas)])
+        return log_prior_ard_batch(thetas, self.prior)
 
     def _normals(self, idx, bufs):
+        t0 = time.perf_counter()
         self.ctx.u_normal(bufs[idx], self.dev_seeds[idx], self.dev_ctr[idx])
+        self.wall['u_draw'] += time.perf_counter() - t0
         self.dev_ctr[idx] += 1
 
     def _theta_eval(self, idx, thetas, slots):
+        """Batched theta-call; returns (log target, log prior) of each proposal."""
+        t0 = time.perf_counter()
         out, st, nops = self.ctx.theta_eval(self.est, thetas, self.ub_u[idx], slots)
+        self.wall['theta_call'] += time.perf_counter() - t0
         self.n_theta_calls += len(idx)
         self.n_cubic_ops[idx] += nops
         bad = st != 0
@@ -106,7 +115,8 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             self.failed[idx[bad]] = True
             self.fail_status[idx[bad]] = st[bad]
             out = np.where(bad, -np.inf, out)
-        return out + self.log_prior(thetas)
+        lp = self.log_prior(thetas)
+        return out + lp, lp
 
     def prior_draw(self):
         """theta_init ~ prior per chain, drawn with each chain's RandomState
@@ -123,7 +133,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         idx = np.arange(self.n_chains)
         self.theta = self.prior_draw() if theta_init is None else np.array(theta_init, float)
         self._normals(idx, self.ub_u)
-        self.log_f = self._theta_eval(idx, self.theta, self.slot_cur[idx])
+        self.log_f, self.lp_cur = self._theta_eval(idx, self.theta, self.slot_cur[idx])
         return self.theta.copy()
 
     # ------------------------------------------------------------------ updates
@@ -150,11 +160,13 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             if it >= self.max_slice_iters:
                 self.failed[act] = True
                 break
+            t0 = time.perf_counter()
             self.ctx.u_combine(self.ub_prop[act], self.ub_u[act], self.ub_nu[act],
                                np.cos(phi[act]), np.sin(phi[act]))
             out, st = self.ctx.u_eval(self.slot_cur[act], self.ub_prop[act])
+            self.wall['u_call'] += time.perf_counter() - t0
             self.n_u_calls += act.size
-            lf = np.where(st == 0, out, -np.inf) + self.log_prior(self.theta[act])
+            lf = np.where(st == 0, out, -np.inf) + self.lp_cur[act]
             keep = []
             for q, c in enumerate(act):
                 if lf[q] > log_y[c]:
@@ -203,7 +215,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             for c in act:
                 x_prop[c] = x_lo[c] + (x_hi[c] - x_lo[c]) * self.prngs[c].uniform()
             th_p = self.theta[act] + x_prop[act, None] * d[act]
-            lf = self._theta_eval(act, th_p, self.slot_prop[act])
+            lf, lp = self._theta_eval(act, th_p, self.slot_prop[act])
             keep = []
             for q, c in enumerate(act):
                 if lf[q] > log_y[c]:
@@ -211,6 +223,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
                     self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
                     self.theta[c] = th_p[q]
                     self.log_f[c] = lf[q]
+                    self.lp_cur[c] = lp[q]
                     continue
                 if self.failed[c]:
                     continue
@@ -238,8 +251,8 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             s = np.zeros(C)
             act = live[(s[live] < budget[live]) & ~self.failed[live]]
             while act.size:
-                lf = self._theta_eval(act, self.theta[act] + ends[act, None] * d[act],
-                                      self.slot_prop[act])
+                lf, _ = self._theta_eval(act, self.theta[act] + ends[act, None] * d[act],
+                                         self.slot_prop[act])
                 inside = log_y[act] < lf
                 grow = act[inside]
                 ends[grow] += sign * self.w
@@ -289,8 +302,9 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             self.prngs[c].uniform()
         self._rd_pend[c] = self.theta[c] + self._rd_x[c] * self._rd_d[c]
 
-    def _rd_result(self, c, lf):
-        """Consume the estimate at chain c's pending theta; True when the transition is done."""
+    def _rd_result(self, c, lf, lp):
+        """Consume the estimate lf (log prior lp) at chain c's pending theta; True when the
+        transition is done."""
         mode = self._rd_mode[c]
         if mode < 2:  # step out while the bracket end is inside the slice (mcmc_updates.py:491-498)
             if self._rd_logy[c] < lf:
@@ -307,6 +321,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
             self.theta[c] = self._rd_pend[c]
             self.log_f[c] = lf
+            self.lp_cur[c] = lp
             return True
         if self.failed[c]:
             return True
@@ -353,9 +368,9 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
             rd = np.flatnonzero(in_rd & ~self.failed)
             if rd.size == 0:
                 break
-            lf = self._theta_eval(rd, self._rd_pend[rd], self.slot_prop[rd])
+            lf, lp = self._theta_eval(rd, self._rd_pend[rd], self.slot_prop[rd])
             for q, c in enumerate(rd):
-                if self._rd_result(c, lf[q]):
+                if self._rd_result(c, lf[q], lp[q]):
                     in_rd[c] = False
                     if not self.failed[c]:
                         done[c] += 1

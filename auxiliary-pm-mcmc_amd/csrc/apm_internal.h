@@ -84,8 +84,13 @@ void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride
 void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
                        int64_t vstride, Live live, int nchains, hipStream_t s);
 // refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
+// acceptance of refinement step `step` on the chains with refining[b] != 0 && status[b] == 0:
+// accepted chains leave the mask; with last = true the others get status = fail_code
 void launch_refine_check(const double* x, const double* d, int64_t vstride, int np, double tol,
-                         int fail_code, Live live, int nchains, hipStream_t s);
+                         int fail_code, int step, bool last, double* prev, int* refining,
+                         const int* status, int nchains, hipStream_t s);
+// refining[b] = chain b live
+void launch_refine_mask(Live live, int* refining, int nchains, hipStream_t s);
 void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,
                    double* out, int64_t vstride, int np, Live live, int nchains, hipStream_t s);
 

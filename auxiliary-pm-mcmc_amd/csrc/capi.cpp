@@ -50,9 +50,12 @@ struct apm_ctx {
     double* sympart = nullptr;  // symmetric K x partials: nb*nb*64 per chain (launch_symv)
     int64_t sstride = 0;
     bool mixed = true;        // APM_MIXED=0: fp64 Newton factorisation (development knob)
-    int n_refine = 1;         // APM_REFINE overrides
-    double refine_tol = 1e-3; // last correction / solution (max norms) accepted by the check
+    int n_refine = 3;         // maximum refinement steps per solve (APM_REFINE overrides)
+    double refine_tol = 1e-3; // acceptance of a refinement step (k_refine_check)
     int *active = nullptr, *status = nullptr, *n_iter = nullptr;
+    int* refining = nullptr;  // chains still refining their Newton solve
+    double* refine_prev = nullptr;  // max|d| of the previous refinement step per chain
+    int64_t n_refine_steps = 0, n_fp64_rerun = 0;  // statistics (apm_prof_read APM_PROF_STATS)
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;
     double *d_ca = nullptr, *d_cb = nullptr;
     uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
@@ -311,28 +314,45 @@ void newton_solve32(apm_ctx* c, int count) {
         launch_trsv_bwd32(F, J, D, ds, r1, c->v.z, vs, lv, count, s);
         check_launch();
     }
-    for (int it = 0; it < c->n_refine; ++it) {
-        launch_refine(0, c->v.Ws, c->v.Kb, c->v.z, nullptr, r2, vs, np, lv, count, s);  // t
+    // fp64 iterative refinement against B = I + W^1/2 K W^1/2, adaptive per chain: a chain
+    // leaves after the step its correction passes k_refine_check; one host read of the mask per
+    // step decides whether another step is launched (usually one step suffices at N=4096)
+    if (c->n_refine > 0) {
+        launch_refine_mask(lv, c->refining, count, s);
         check_launch();
-        launch_symv(c->K, r2, vs, r3, vs, c->sympart, c->sstride, np, MatF{}, nullptr, 0, lv,
+    }
+    const Live lr{c->refining, c->status};
+    std::vector<int> ref_h(count);
+    for (int it = 0; it < c->n_refine; ++it) {
+        launch_refine(0, c->v.Ws, c->v.Kb, c->v.z, nullptr, r2, vs, np, lr, count, s);  // t
+        check_launch();
+        launch_symv(c->K, r2, vs, r3, vs, c->sympart, c->sstride, np, MatF{}, nullptr, 0, lr,
                     count, s);                                                           // K t
         check_launch();
-        launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lv, count, s);       // res
+        launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lr, count, s);       // res
         check_launch();
         for (int J = 0; J < nb; ++J) {
-            launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lv, count, s);
+            launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lr, count, s);
             check_launch();
         }
         for (int J = nb - 1; J >= 0; --J) {
-            launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lv, count, s);
+            launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lr, count, s);
             check_launch();
         }
-        if (it + 1 == c->n_refine) {  // accept only a converged refinement (else: fp64 rerun)
-            launch_refine_check(c->v.z, r3, vs, np, c->refine_tol, APM_STATUS_CHOL_B, lv, count, s);
-            check_launch();
-        }
-        launch_refine(2, nullptr, nullptr, c->v.z, nullptr, r3, vs, np, lv, count, s);  // x += d
+        launch_refine(2, nullptr, nullptr, c->v.z, nullptr, r3, vs, np, lr, count, s);  // x += d
         check_launch();
+        const bool last = it + 1 == c->n_refine;
+        launch_refine_check(c->v.z, r3, vs, np, c->refine_tol, APM_STATUS_CHOL_B, it, last,
+                            c->refine_prev, c->refining, c->status, count, s);
+        check_launch();
+        ++c->n_refine_steps;
+        if (last) break;
+        HIPC(hipMemcpyAsync(ref_h.data(), c->refining, sizeof(int) * count,
+                            hipMemcpyDeviceToHost, s));
+        sync(c);
+        bool any = false;
+        for (int b = 0; b < count; ++b) any |= ref_h[b] != 0;
+        if (!any) break;
     }
 }
 
@@ -409,6 +429,7 @@ void newton_is(apm_ctx* c, int count, std::vector<int>& st_h) {
     for (int b = 0; b < count; ++b)
         if (st_h[b] == APM_STATUS_CHOL_B) redo.push_back(b);
     if (redo.empty()) return;
+    c->n_fp64_rerun += (int64_t)redo.size();
     std::vector<int> nit(count);
     HIPC(hipMemcpyAsync(nit.data(), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
                         c->stream));
@@ -546,6 +567,15 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->device = device;
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
     if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
+    if (const char* e = getenv("APM_SCHED")) {  // host wait policy of synchronisations
+        const std::string m(e);
+        const unsigned f = m == "spin" ? hipDeviceScheduleSpin
+                         : m == "yield" ? hipDeviceScheduleYield
+                         : m == "block" ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+        (void)hipSetDevice(device);
+        (void)hipSetDeviceFlags(f);  // fails harmlessly once the device is active
+        (void)hipGetLastError();
+    }
     HIPC(hipSetDevice(device));
     if (const char* e = getenv("APM_FUSE_DIAG")) c->fuse_diag = atoi(e) != 0;
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
@@ -600,6 +630,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->active = dalloc<int>(c, B);
     c->status = dalloc<int>(c, B);
     c->n_iter = dalloc<int>(c, B);
+    c->refining = dalloc<int>(c, B);
+    c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, B);
     c->d_ubufs = dalloc<int64_t>(c, B);
     c->d_i3 = dalloc<int64_t>(c, 3 * B);
@@ -1039,6 +1071,13 @@ int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, dou
     try {
         HIPC(hipSetDevice(c->device));
         sync(c);
+        if (kind == APM_PROF_STATS) {
+            if (total_ms) *total_ms = 0.0;
+            if (launches) *launches = c->n_fp64_rerun;
+            if (work) *work = (double)c->n_refine_steps;
+            if (reset) c->n_fp64_rerun = c->n_refine_steps = 0;
+            return APM_SUCCESS;
+        }
         double ms = 0.0, wk = 0.0;
         int64_t cnt = 0;
         for (const ProfRec& r : c->recs) {

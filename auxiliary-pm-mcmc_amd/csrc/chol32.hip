@@ -1,9 +1,10 @@
 // Mixed-precision Newton solve: B = I + W^1/2 K W^1/2 factored in fp32 (f32 MFMA), the solve
-// B x = W^1/2 K b refined once against the fp64 B.
+// B x = W^1/2 K b refined against the fp64 B until the per-chain acceptance test passes
+// (usually one step at N=4096; up to APM_REFINE = 3 steps, e.g. at N=16384).
 //
 // The reference factors B in fp64 at every Newton iteration (latent_posterior_approximations.py:92)
 // and solves with it (:94). B's eigenvalues are >= 1 and its condition number is ~1 + max(W) *
-// lambda_max(K), so the fp32 factor solves to ~cond * 6e-8 and ONE step of iterative refinement
+// lambda_max(K), so the fp32 factor solves to ~cond * 6e-8 and a step of iterative refinement
 // with the fp64 residual r = rhs - x - W^1/2 (K (W^1/2 x)) brings x to fp64 accuracy (measured
 // Newton modes agree with the all-fp64 iteration to 1e-12 relative for typical theta and 1e-8 at
 // sigma = e^4; tests/test_gpu_kernels.py checks the mode against the oracle). The IS estimator
@@ -465,14 +466,19 @@ __global__ __launch_bounds__(256) void k_refine(int mode, const double* __restri
         out[o] = 0.0;
 }
 
-// Acceptance test of the refined solve: the last correction d must be small against x
-// (max|d| <= tol * max|x|; the refined error is then ~ (tol)^2 relative). Otherwise the fp32
-// factor is too inaccurate for this chain (extreme theta) and status = fail_code sends the chain
-// to the fp64 rerun (capi.cpp newton_is).
+// Acceptance test of refinement step `step` (0-based), run after x += d on the chains still
+// refining (live.active = the refining mask). The error left after a correction d_k is about
+// rho |d_k| with the contraction rho ~ |d_k| / |d_{k-1}| (d_0 = the first solve x), so a chain
+// is accepted when max|d_k|^2 <= tol^2 max|x| max|d_{k-1}| — for the first step exactly
+// max|d| <= tol max|x| (refined error ~ tol^2 relative). Accepted chains leave the refining mask;
+// after the last allowed step the others get status = fail_code, which sends them to the fp64
+// rerun (capi.cpp newton_is): the fp32 factor is too inaccurate for them (extreme theta).
+// prev[b] keeps max|d_{k-1}|.
 __global__ __launch_bounds__(256) void k_refine_check(const double* __restrict__ x,
                                                       const double* __restrict__ d,
                                                       int64_t vstride, int np, double tol,
-                                                      int fail_code, Live live) {
+                                                      int fail_code, int step, int last,
+                                                      double* prev, int* refining, Live live) {
     const int b = blockIdx.x;
     if (!live32(live, b)) return;
     double mx = 0.0, md = 0.0;
@@ -491,13 +497,33 @@ __global__ __launch_bounds__(256) void k_refine_check(const double* __restrict__
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0 && !(sd[0] <= tol * sx[0])) live.status[b] = fail_code;
+    if (threadIdx.x == 0) {
+        const double pm = step == 0 ? sx[0] : prev[b];
+        if (sd[0] * sd[0] <= tol * tol * sx[0] * pm)
+            refining[b] = 0;  // converged: leaves the refining mask (live.active == refining)
+        else if (last)
+            live.status[b] = fail_code;
+        else
+            prev[b] = sd[0];
+    }
 }
 
 void launch_refine_check(const double* x, const double* d, int64_t vstride, int np, double tol,
-                         int fail_code, Live live, int nchains, hipStream_t s) {
+                         int fail_code, int step, bool last, double* prev, int* refining,
+                         const int* status, int nchains, hipStream_t s) {
     hipLaunchKernelGGL(k_refine_check, dim3(nchains), dim3(256), 0, s, x, d, vstride, np, tol,
-                       fail_code, live);
+                       fail_code, step, (int)last, prev, refining,
+                       Live{refining, const_cast<int*>(status)});
+}
+
+__global__ void k_refine_mask(Live live, int* refining, int nchains) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nchains) refining[b] = live32(live, b) ? 1 : 0;
+}
+
+void launch_refine_mask(Live live, int* refining, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_refine_mask, dim3((nchains + 255) / 256), dim3(256), 0, s, live,
+                       refining, nchains);
 }
 
 void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,

@@ -9,7 +9,8 @@ import numpy as np
 from scipy.special import gammaln
 
 __all__ = ['gamma_log_pdf', 'log_gamma_log_pdf', 'adapt_factor_func', 'normalise_inputs',
-           'save_run', 'save_adaptive_run', 'plot_trace', 'log_prior_ard', 'synthetic_gp_data']
+           'save_run', 'save_adaptive_run', 'plot_trace', 'log_prior_ard', 'log_prior_ard_batch',
+           'synthetic_gp_data', 'load_uci_data']
 
 
 def gamma_log_pdf(x, a, b):
@@ -42,6 +43,43 @@ def log_prior_ard(theta, prior):
     lp = log_gamma_log_pdf(theta[0], prior['a_sigma'], prior['b_sigma'])
     for k in range(1, len(theta)):
         lp += log_gamma_log_pdf(theta[k], prior['a_tau'], prior['b_tau'])
+    return lp
+
+
+def load_uci_data(data_set, data_dir=None, normalise=True):
+    """Load `<data_dir>/<data_set>_X.txt` and `_y.txt` the way every experiment notebook does
+    (e.g. E-SS+RD-SS.ipynb cells at :85-87: np.genfromtxt, then normalise_inputs on X).
+    `data_dir` defaults to $DATA_DIR/uci (notebook :39). Returns (X, y) or, with
+    normalise=True, (X_normalised, y, X_mn, X_sd). Labels must be +-1 (probit likelihood);
+    a ValueError names the offending file otherwise."""
+    if data_dir is None:
+        data_dir = os.path.join(os.environ['DATA_DIR'], 'uci')
+    x_path = os.path.join(data_dir, data_set + '_X.txt')
+    y_path = os.path.join(data_dir, data_set + '_y.txt')
+    X = np.genfromtxt(x_path)
+    y = np.genfromtxt(y_path)
+    if X.ndim == 1:
+        X = X[:, None]
+    if y.ndim != 1 or y.shape[0] != X.shape[0]:
+        raise ValueError('{0}: {1} labels for {2} inputs'.format(y_path, y.size, X.shape[0]))
+    if not np.all((y == 1.) | (y == -1.)):
+        raise ValueError('{0}: labels must be +1/-1'.format(y_path))
+    if not normalise:
+        return X, y
+    X, X_mn, X_sd = normalise_inputs(X)
+    return X, y, X_mn, X_sd
+
+
+def log_prior_ard_batch(thetas, prior):
+    """log_prior_ard of every row of `thetas` (chains x P) at once: the same terms, summed in
+    the same order (theta[0] term, then += each length-scale term), vectorised over chains so a
+    64-chain batch costs microseconds of host time instead of milliseconds."""
+    th = np.atleast_2d(np.asarray(thetas, dtype=np.float64))
+    lp = log_gamma_log_pdf(th[:, 0], prior['a_sigma'], prior['b_sigma'])
+    if th.shape[1] > 1:
+        terms = log_gamma_log_pdf(th[:, 1:], prior['a_tau'], prior['b_tau'])
+        for k in range(terms.shape[1]):
+            lp = lp + terms[:, k]
     return lp
 
 

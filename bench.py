@@ -198,11 +198,13 @@ def main():
         for _ in range(a.warmup):
             smp.step()
     ctx = smp.ctx
-    for k in (0, 1, 2, 3):
+    for k in (0, 1, 2, 3, 4):
         ctx.prof_read(k, reset=True)
     ctx.prof_enable(True)
     ctx.prof_marker(1)  # timed-region brackets for rocprofv3 traces (tools/prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
+    for k in smp.wall:
+        smp.wall[k] = 0.
     res = {}
     if a.schedule == 'async':
         # every chain completes >= K transitions; chains that are ahead keep working until the
@@ -234,6 +236,7 @@ def main():
     for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32')):
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
+    _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
 
     def mfma_roofline(name, kernel, peak, short):
         ms, cnt, flops = prof[name]
@@ -313,6 +316,9 @@ def main():
         'schedule': a.schedule, 'transitions_timed': int(transitions),
         'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
         'failed_chains': int(dist.sum(int(smp.failed.sum()))),
+        'newton_refinement_steps': int(dist.sum(n_refine)),
+        'newton_fp64_reruns': int(dist.sum(n_rerun)),
+        'wall_split_s': dict(smp.wall, host_sampler=elapsed - sum(smp.wall.values())),
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)

@@ -116,7 +116,9 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
 #define APM_PROF_CHOL_UPDATE 1
 #define APM_PROF_UGEMM 2
 #define APM_PROF_CHOL_UPDATE32 3
-#define APM_PROF_NKINDS 4
+#define APM_PROF_STATS 4 /* not a kernel: launches = chains whose mixed-precision Newton solve was
+                            rerun in fp64, work = refinement steps launched, total_ms = 0 */
+#define APM_PROF_NKINDS 5
 int apm_prof_enable(apm_ctx *ctx, int on);
 /* total device milliseconds and launch count per tracked kernel since the last reset; also the
  * algorithmic work: bytes (GRAM) or flops (CHOL_UPDATE, CHOL_UPDATE32 = the fp32 Newton

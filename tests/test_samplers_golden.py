@@ -176,3 +176,35 @@ def test_save_run_schema(tmp_path):
     z = np.load(res)
     assert set(z.files) == {'adapt_thetas', 'adapt_prop_scales', 'adapt_accept_rates', 'thetas',
                             'n_reject_n_cubic_ops_comp_time'}
+
+
+def test_load_uci_data(tmp_path, monkeypatch):
+    """Notebook data path (E-SS+RD-SS.ipynb :39, :85-87): $DATA_DIR/uci/<set>_{X,y}.txt read with
+    genfromtxt, X normalised with normalise_inputs."""
+    u = golden('utils')
+    uci = tmp_path / 'uci'
+    uci.mkdir()
+    y = np.where(np.arange(u['Xraw'].shape[0]) % 3 == 0, 1., -1.)
+    np.savetxt(str(uci / 'toy_X.txt'), u['Xraw'])
+    np.savetxt(str(uci / 'toy_y.txt'), y)
+    monkeypatch.setenv('DATA_DIR', str(tmp_path))
+    X, yy, mn, sd = utils.load_uci_data('toy')
+    np.testing.assert_allclose(X, u['Xn'], rtol=1e-14, atol=1e-14)
+    np.testing.assert_allclose(mn, u['mn'], rtol=1e-14)
+    np.testing.assert_array_equal(yy, y)
+    Xr, _ = utils.load_uci_data('toy', str(uci), normalise=False)
+    np.testing.assert_allclose(Xr, u['Xraw'], rtol=1e-15)
+    np.savetxt(str(uci / 'bad_X.txt'), u['Xraw'])
+    np.savetxt(str(uci / 'bad_y.txt'), np.abs(y) * 0.)
+    with pytest.raises(ValueError):
+        utils.load_uci_data('bad', str(uci))
+
+
+def test_log_prior_ard_batch_matches_scalar():
+    """The batched sampler's vectorised prior equals the notebook closure's per-theta sum."""
+    prior = dict(a_tau=1., b_tau=1. / 32 ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    th = np.random.RandomState(0).normal(scale=2., size=(64, 33))
+    ref = np.array([utils.log_prior_ard(t, prior) for t in th])
+    np.testing.assert_allclose(utils.log_prior_ard_batch(th, prior), ref, rtol=1e-14, atol=1e-12)
+    np.testing.assert_allclose(utils.log_prior_ard_batch(th[:, :2], prior),
+                               [utils.log_prior_ard(t, prior) for t in th[:, :2]], rtol=1e-14)
