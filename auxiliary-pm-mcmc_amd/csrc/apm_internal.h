@@ -51,6 +51,10 @@ struct FusedDiag {
 void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
                         Live live, int nchains, hipStream_t s,
                         FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
+// the same with one 128x128 super-tile per workgroup (tiles from build_update_supertiles)
+void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+                             Live live, int nchains, hipStream_t s,
+                             FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo = 0, int ghi = 0);
@@ -71,6 +75,11 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0});
+// the same update with one 128x128 super-tile per workgroup (tiles from build_update_supertiles)
+void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
+                               Live live, int nchains, hipStream_t s,
+                               FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0});
+std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi);
 // y = K x from K's lower tiles (part: nb*nb*64 doubles per chain of partials); Bf.base != null
 // also forms the fp32 Newton matrix I + W^1/2 K W^1/2 and its right-hand-side block (x = b)
 void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,

@@ -71,6 +71,10 @@ struct apm_ctx {
     std::vector<ProfRec> recs;
     // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
+    std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
+    // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
+    int t128 = 3;
+    bool left_inner = true;  // left-looking updates inside an outer panel (APM_LEFT=0: right)
 };
 
 namespace {
@@ -127,14 +131,14 @@ struct ProfScope {
     hipEvent_t a{}, b{};
     ProfScope(apm_ctx* c_, int k, double w, hipStream_t s_ = nullptr)
         : c(c_), kind(k), work(w), s(s_ ? s_ : c_->stream) {
-        if (c->prof) {
+        if (c->prof && kind >= 0) {
             a = next_event(c);
             b = next_event(c);
             HIPC(hipEventRecord(a, s));
         }
     }
     ~ProfScope() {
-        if (c->prof && hipEventRecord(b, s) == hipSuccess)
+        if (c->prof && kind >= 0 && hipEventRecord(b, s) == hipSuccess)
             c->recs.push_back(ProfRec{a, b, kind, work});
     }
 };
@@ -148,7 +152,7 @@ Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
 // rank-256 update per outer panel (4x less read-modify-write traffic than rank-64 steps).
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
-static int OUTER = 4;  // tiles per outer panel (APM_OUTER overrides, development knob)
+static int OUTER = 8;  // tiles per outer panel (APM_OUTER overrides, development knob)
 
 // Row tiles [lo, hi) known to be zero in panel column k (skipped by panel and update).
 struct Gap {
@@ -186,6 +190,8 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
 // Trailing update of tiles (i, j), i in [i0, R) minus the gap, j in [j0, min(i, jend-1)], by
 // columns [k0, k0+kc). fuse_k >= 0: the launch also factors diagonal tile (fuse_k, fuse_k), which
 // must be its first tile (i0 == j0 == fuse_k; the super-tile order starts there).
+std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g);
+
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
                     bool plus, int count, int fuse_k = -1, int fail_code = 0) {
     if (i0 < j0) i0 = j0;
@@ -194,9 +200,16 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     if (tl.second <= 0) return;
     FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0) fd = FusedDiag<double>{1, c->Dinv, c->dstride, c->ldet, c->lstride, fail_code};
-    ProfScope ps(c, APM_PROF_CHOL_UPDATE,
-                 c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0);
-    launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream, fd);
+    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0;
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl);
+    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl);
+    if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
+        const auto sl = super_list(c, i0, R, j0, jend, g);
+        launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, live_of(c), count,
+                                c->stream, fd);
+    } else {
+        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream, fd);
+    }
     check_launch();
 }
 
@@ -215,6 +228,28 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
     bool have_diag = false;  // tile (k, k) already factored by the previous update launch
     for (int K = k0; K < k1; K += OUTER) {
         const int Kend = std::min(K + OUTER, k1);
+        if (fuse && c->left_inner) {
+            // left-looking inside the outer panel: column k receives all of the panel's earlier
+            // columns in ONE update (depth (k-K)*64, one read-modify-write of its tiles instead
+            // of k-K), whose first tile is the diagonal tile it then factors (fused diag)
+            for (int k = K; k < Kend; ++k) {
+                const Gap g = gap(k, c->nb);
+                if (k > K)
+                    tracked_update(c, M, K, k - K, k, R, k, k + 1, g, false, count, k, fail_code);
+                else if (!have_diag) {
+                    launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv,
+                                     fail_code, count, c->stream);
+                    check_launch();
+                }
+                launch_chol_panel(M, k, k + 1, R, g.lo, g.hi, c->Dinv, c->dstride, lv, count,
+                                  c->stream);
+                check_launch();
+            }
+            have_diag = Kend < k1;
+            tracked_update(c, M, K, Kend - K, Kend, R, Kend, Cb, gap(Kend - 1, c->nb), false,
+                           count, have_diag ? Kend : -1, fail_code);
+            continue;
+        }
         for (int k = K; k < Kend; ++k) {
             if (factor_diag && !have_diag) {
                 launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
@@ -241,6 +276,18 @@ MatF b32_of(apm_ctx* c) {
 }
 float* dinv32_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv); }
 
+std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g) {
+    auto key = std::make_tuple(i0, R, j0, jend, g.lo, g.hi);
+    auto it = c->super_lists.find(key);
+    if (it != c->super_lists.end()) return it->second;
+    std::vector<unsigned> v = build_update_supertiles(i0, R, j0, jend, g.lo, g.hi);
+    unsigned* d = dalloc<unsigned>(c, v.size());
+    HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
+    auto val = std::make_pair(d, (int)v.size());
+    c->super_lists[key] = val;
+    return val;
+}
+
 void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
                       int count, int fuse_k = -1, int fail_code = 0) {
     if (i0 < j0) i0 = j0;
@@ -250,9 +297,16 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0)
         fd = FusedDiag<float>{1, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, fail_code};
-    ProfScope ps(c, APM_PROF_CHOL_UPDATE32,
-                 c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * count : 0.0);
-    launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd);
+    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * count : 0.0;
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
+    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl);
+    if ((c->t128 & 1) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
+        const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0});
+        launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
+                                  fd);
+    } else {
+        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd);
+    }
     check_launch();
 }
 
@@ -264,6 +318,23 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     bool have_diag = false;
     for (int K = k0; K < k1; K += OUTER) {
         const int Kend = std::min(K + OUTER, k1);
+        if (c->fuse_diag && c->left_inner) {  // left-looking inside the panel (chol_range)
+            for (int k = K; k < Kend; ++k) {
+                if (k > K)
+                    tracked_update32(c, M, K, k - K, k, R, k, k + 1, count, k, fail_code);
+                else if (!have_diag) {
+                    launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
+                                       c->stream);
+                    check_launch();
+                }
+                launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
+                check_launch();
+            }
+            have_diag = Kend < k1;
+            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
+                             fail_code);
+            continue;
+        }
         for (int k = K; k < Kend; ++k) {
             if (!have_diag) {
                 launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
@@ -581,6 +652,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
+    if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
+    if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->kind = kind;
     c->n = (int)n;

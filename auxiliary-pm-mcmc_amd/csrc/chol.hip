@@ -359,6 +359,185 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
                        ntiles, nchains, (int)plus, live, fd);
 }
 
+// ------------------------------------------------------------------------- 128x128 trailing update
+// The fp64 twin of chol32.hip's k_chol_update32_t128 (super-tile entries and validity rules of
+// build_update_supertiles): one 128x128 super-tile per workgroup, each wave a 64x64 tile as 4x4
+// v_mfma_f64_16x16x4_f64 accumulators (128 VGPRs). Per byte staged it feeds twice the MFMAs of the
+// 64x64 kernel, whose operand-load rate co-limits it. Operands move global -> LDS with 16-byte
+// LDS-DMA loads (global_load_lds_dwordx4: no staging registers, no ds_write pass), two buffers of
+// KS = 16-deep slices; the LDS image is lane-linear per wave (8 rows of 128 B per instruction)
+// with the 16-byte pieces XOR-swizzled by row (piece p of row r at slot p ^ (r & 7)), so the
+// 16-byte fragment reads of 8 consecutive rows hit distinct banks.
+#define KS64T 16
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+struct __attribute__((aligned(16))) GemmSmem64T {
+    double a[2][128][KS64T];
+    double b[2][128][KS64T];
+};
+
+template <bool NEG>
+__device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigned e, int b,
+                                                 bool fused, Live live, FusedDiag<double> fd,
+                                                 GemmSmem64T& smg, DiagSmem& smd) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int ti = (int)(e >> 18), tj = (int)((e >> 4) & 0x3fff);
+    const bool rv0 = e & 1u, rv1 = e & 2u, cv0 = e & 4u, cv1 = e & 8u;
+    const int ra0 = rv0 ? ti : ti + 1, ra1 = rv1 ? ti + 1 : ti;
+    const int cb0 = cv0 ? tj : tj + 1, cb1 = cv1 ? tj + 1 : tj;
+    double* Ab = A.base + b * A.cstride;
+    const int oi = ti + wr, oj = tj + wc;
+    const bool mine = (wr ? rv1 : rv0) && (wc ? cv1 : cv0) && oj <= oi;
+
+    // LDS-DMA staging: wave wv moves operand rows 32wv .. 32wv+31 (4 instructions of 8 rows);
+    // lane l takes row +l/8 and stores slot l%8, i.e. global piece (l%8) ^ (l/8)
+    const int srow = 32 * wv + (lane >> 3);  // < 64 for waves 0,1 (first half), else second
+    const int spiece = (lane & 7) ^ (lane >> 3);
+    const int64_t ld8 = 8 * A.ld;
+    const double* ga = Ab + (int64_t)((wv < 2 ? ra0 : ra1) * 64 + (srow & 63)) * A.ld + k0 * 64 +
+                       2 * spiece;
+    const double* gb = Ab + (int64_t)((wv < 2 ? cb0 : cb1) * 64 + (srow & 63)) * A.ld + k0 * 64 +
+                       2 * spiece;
+    auto glds = [&](int sidx, int buf) {
+        const int o = sidx * KS64T;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_global_load_lds((glb_void_t*)(ga + q * ld8 + o),
+                                             (lds_void_t*)&smg.a[buf][32 * wv + 8 * q][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_void_t*)(gb + q * ld8 + o),
+                                             (lds_void_t*)&smg.b[buf][32 * wv + 8 * q][0], 16, 0, 0);
+        }
+    };
+    d4_t acc[4][4];
+    // lane group kq takes the slice's k values 4kq .. 4kq+3 (the same k for A and B): a lane's
+    // fragments of two MFMA steps are one 16-byte LDS read (piece 2kq+h, swizzled by row)
+    auto compute = [&](int cur) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int slot = ((2 * kq + h) ^ (r16 & 7)) * 2;
+            d2_t a2[4], b2[4];
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi)
+                a2[bi] = *reinterpret_cast<const d2_t*>(&smg.a[cur][64 * wr + 16 * bi + r16][slot]);
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+                b2[bj] = *reinterpret_cast<const d2_t*>(&smg.b[cur][64 * wc + 16 * bj + r16][slot]);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 4; ++bj)
+                        acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            a2[bi][q], b2[bj][q], acc[bi][bj], 0, 0, 0);
+        }
+    };
+    const int nsub = (64 * kc) / KS64T;
+    // old tile into acc (negated for A_ij -= ...: acc = -C + sum, result = -acc), consumed before
+    // the loop so that no wait for it lands inside (see k_chol_update32_t128)
+    const int li = mine ? oi : (wr ? ra1 : ra0), lj = mine ? oj : (wc ? cb1 : cb0);
+    const double* Cw = Ab + (int64_t)(li * 64) * A.ld + lj * 64;
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double v = Cw[(int64_t)(16 * bi + F64_CROW(lane, r)) * A.ld + 16 * bj + r16];
+                acc[bi][bj][r] = NEG ? -v : v;
+            }
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) asm volatile("" : "+v"(acc[bi][bj]));
+    glds(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nsub; ++s) {
+        if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
+        compute(s & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (NEG) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj) acc[bi][bj] = -acc[bi][bj];
+    }
+    double* Cout = Ab + (int64_t)(oi * 64) * A.ld + oj * 64;
+    const bool diag_here = fused && wv == 0;
+    if (mine && !diag_here) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    Cout[(int64_t)(16 * bi + F64_CROW(lane, r)) * A.ld + 16 * bj + r16] =
+                        acc[bi][bj][r];
+    }
+    if (!fused) return;
+    if (wv == 0) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    smd.T[(16 * bi + F64_CROW(lane, r)) * DP + 16 * bj + r16] = acc[bi][bj][r];
+    }
+    __syncthreads();
+    if (wv == 0) {  // rolled pivot loops (register budget), as in k_chol_update
+        const bool ok = diag_compute<false>(smd, lane);
+        if (lane == 0) smd.ok = ok;
+    }
+    __syncthreads();
+    if (!smd.ok) {
+        if (tid == 0) live.status[b] = fd.fail_code;
+        return;
+    }
+    diag_store<double>(smd, Ab + (int64_t)(ti * 64) * A.ld + tj * 64, A.ld,
+                       fd.Dinv + b * fd.dstride + (int64_t)ti * 4096, fd.ldet + b * fd.lstride + ti,
+                       tid, 256);
+}
+
+__global__ __launch_bounds__(256, 2) void k_chol_update_t128(MatB A, int k0, int kc,
+                                                             const unsigned* __restrict__ tiles,
+                                                             int ntiles, int nchains, int plus,
+                                                             Live live, FusedDiag<double> fd) {
+    __shared__ union {
+        GemmSmem64T g;
+        DiagSmem d;
+    } sm;
+    int b, t;
+    const bool fused = fd.enabled && (int)blockIdx.x < nchains;
+    if (fused) {
+        b = blockIdx.x;
+        t = 0;
+    } else {
+        const int nt = fd.enabled ? ntiles - 1 : ntiles;
+        const long L = (long)blockIdx.x - (fd.enabled ? nchains : 0);
+        const long w = xcd_remap(L, (long)nt * nchains);
+        b = (int)(w / nt);
+        t = (int)(w % nt) + (fd.enabled ? 1 : 0);
+    }
+    if (!chain_live(live, b)) return;
+    if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
+        update_t128_body<false>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+    else
+        update_t128_body<true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+}
+
+void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+                             Live live, int nchains, hipStream_t s, FusedDiag<double> fd) {
+    if (ntiles <= 0) return;
+    const long total = (long)ntiles * nchains;
+    hipLaunchKernelGGL(k_chol_update_t128, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc,
+                       tiles, ntiles, nchains, (int)plus, live, fd);
+}
+
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
 // super-rows top-down, super-columns left-right, row-major inside), packed (i << 16) | j.
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo, int ghi) {

@@ -245,6 +245,231 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
                        ntiles, nchains, live, fd);
 }
 
+// ------------------------------------------------------------------------- 128x128 trailing update
+// The rank-64*kc outer updates with one 128x128 super-tile (2x2 tiles) per workgroup: each wave
+// owns a 64x64 tile (4x4 v_mfma_f32_16x16x4_f32 accumulators), so a slice of operands staged in
+// LDS feeds twice the MFMAs of the 64x64 kernel per byte loaded (8 instead of 16 B/clk/CU of
+// L2->LDS traffic at the MFMA rate: the 64x64 kernel is operand-load bound).
+// Super-tile entries (build_update_supertiles): (i << 18) | (j << 4) | rv0 | rv1<<1 | cv0<<2 |
+// cv1<<3, rows i, i+1 and columns j, j+1 (tile units) with per-half validity; a tile (i+a, j+b)
+// is written iff rv_a && cv_b && j+b <= i+a. Invalid halves load a valid half's operands (no
+// out-of-range reads) and their results are dropped.
+#ifndef T128_ABL
+#define T128_ABL 0
+#endif
+#define KS128 32
+#define LP128 (KS128 + 4)  // 144-byte rows: the 16-byte fragment reads of 8 row-consecutive
+                           // lanes cover all 32 banks (conflict-free ds_read_b128)
+struct __attribute__((aligned(16))) GemmSmem128 {
+    float a[2][128][LP128];
+    float b[2][128][LP128];
+};
+
+__global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
+                                                               const unsigned* __restrict__ tiles,
+                                                               int ntiles, int nchains, Live live,
+                                                               FusedDiag<float> fd) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    __shared__ union {
+        GemmSmem128 g;
+        DiagSmem d;
+    } sm;
+    int b, t;
+    const bool fused = fd.enabled && (int)blockIdx.x < nchains;
+    if (fused) {
+        b = blockIdx.x;
+        t = 0;
+    } else {
+        const int nt = fd.enabled ? ntiles - 1 : ntiles;
+        const long L = (long)blockIdx.x - (fd.enabled ? nchains : 0);
+        const long w = xcd_remap32(L, (long)nt * nchains);
+        b = (int)(w / nt);
+        t = (int)(w % nt) + (fd.enabled ? 1 : 0);
+    }
+    if (!live32(live, b)) return;
+    const unsigned e = tiles[t];
+    const int ti = (int)(e >> 18), tj = (int)((e >> 4) & 0x3fff);
+    const bool rv0 = e & 1u, rv1 = e & 2u, cv0 = e & 4u, cv1 = e & 8u;
+    // operand row tiles of the two halves (an invalid half reuses the valid one)
+    const int ra0 = rv0 ? ti : ti + 1, ra1 = rv1 ? ti + 1 : ti;
+    const int cb0 = cv0 ? tj : tj + 1, cb1 = cv1 ? tj + 1 : tj;
+    float* Ab = A.base + b * A.cstride;
+    // this wave's output tile
+    const int oi = ti + wr, oj = tj + wc;
+    const bool mine = (wr ? rv1 : rv0) && (wc ? cv1 : cv0) && oj <= oi;
+
+    constexpr int PPR = KS128 / 4;        // 16-byte pieces per slice row
+    constexpr int PPT = 128 * PPR / 256;  // pieces per thread per operand (4)
+    const float* arow[PPT];
+    const float* brow[PPT];
+    int prow[PPT], pcol[PPT];
+#pragma unroll
+    for (int h = 0; h < PPT; ++h) {
+        const int p = tid + 256 * h;
+        prow[h] = p / PPR;
+        pcol[h] = (p % PPR) * 4;
+        const int rt = prow[h] < 64 ? ra0 : ra1, ct = prow[h] < 64 ? cb0 : cb1;
+        arow[h] = Ab + (int64_t)(rt * 64 + (prow[h] & 63)) * A.ld + k0 * 64 + pcol[h];
+        brow[h] = Ab + (int64_t)(ct * 64 + (prow[h] & 63)) * A.ld + k0 * 64 + pcol[h];
+    }
+    auto gload = [&](int sidx, f4_t (&ra)[PPT], f4_t (&rb)[PPT]) {
+#if T128_ABL == 1  // ablation (tools/upd32_bench.cpp): operands always slice 0 (cache resident)
+        sidx = 0;
+#endif
+#if T128_ABL == 3  // ablation: no operand loads
+        return;
+#endif
+#pragma unroll
+        for (int h = 0; h < PPT; ++h) {
+            ra[h] = *reinterpret_cast<const f4_t*>(arow[h] + sidx * KS128);
+            rb[h] = *reinterpret_cast<const f4_t*>(brow[h] + sidx * KS128);
+        }
+    };
+    auto sstore = [&](int buf, const f4_t (&ra)[PPT], const f4_t (&rb)[PPT]) {
+#if T128_ABL == 3
+        return;
+#endif
+#pragma unroll
+        for (int h = 0; h < PPT; ++h) {  // A_ij -= A_ik A_jk^T
+            *reinterpret_cast<f4_t*>(&sm.g.a[buf][prow[h]][pcol[h]]) = -ra[h];
+            *reinterpret_cast<f4_t*>(&sm.g.b[buf][prow[h]][pcol[h]]) = rb[h];
+        }
+    };
+    f4_t acc[4][4];
+    // lane group kq takes the slice's k values 8kq .. 8kq+7 (the same k for A and B, so every k
+    // is summed once): a lane's fragments for 4 MFMA steps are one 16-byte LDS read
+    auto compute = [&](int cur) {
+#pragma unroll
+        for (int h = 0; h < KS128 / 16; ++h) {
+            f4_t a4[4], b4[4];
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi)
+                a4[bi] = *reinterpret_cast<const f4_t*>(
+                    &sm.g.a[cur][64 * wr + 16 * bi + r16][8 * kq + 4 * h]);
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+                b4[bj] = *reinterpret_cast<const f4_t*>(
+                    &sm.g.b[cur][64 * wc + 16 * bj + r16][8 * kq + 4 * h]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 4; ++bj)
+#if T128_ABL == 2  // ablation: no MFMA (loads + LDS + barriers only)
+                        acc[bi][bj][0] += a4[bi][q] * b4[bj][q];
+#else
+                        acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            a4[bi][q], b4[bj][q], acc[bi][bj], 0, 0, 0);
+#endif
+        }
+    };
+    const int nsub = (64 * kc) / KS128;  // even
+    f4_t ra0v[PPT], rb0v[PPT], ra1v[PPT], rb1v[PPT];
+    // old tile (this wave's output, or a valid tile when the output is dropped) into acc, issued
+    // before the operand loads and consumed (empty asm) before the loop: otherwise the compiler's
+    // wait for it sits inside the loop and drains the operand prefetch every iteration
+    const int li = mine ? oi : (wr ? ra1 : ra0), lj = mine ? oj : (wc ? cb1 : cb0);
+    const float* Cw = Ab + (int64_t)(li * 64) * A.ld + lj * 64;
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[bi][bj][r] = Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
+    gload(0, ra0v, rb0v);
+    gload(1, ra1v, rb1v);
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) asm volatile("" : "+v"(acc[bi][bj]));
+    sstore(0, ra0v, rb0v);
+    __syncthreads();
+    for (int s = 0; s < nsub; s += 2) {
+        gload(min(s + 2, nsub - 1), ra0v, rb0v);
+        compute(0);
+        sstore(1, ra1v, rb1v);
+        __syncthreads();
+        gload(min(s + 3, nsub - 1), ra1v, rb1v);
+        compute(1);
+        sstore(0, ra0v, rb0v);
+        __syncthreads();
+    }
+    float* Cout = Ab + (int64_t)(oi * 64) * A.ld + oj * 64;
+    const bool diag_here = fused && wv == 0;  // tile (ti, tj) = (d, d) goes through the diag step
+    if (mine && !diag_here) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    Cout[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16] =
+                        acc[bi][bj][r];
+    }
+    if (!fused) return;
+    // the GEMM loop ended on a barrier: the staging area is free for the diag working set
+    if (wv == 0) {
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sm.d.T[(16 * bi + F32_CROW(lane, r)) * DP + 16 * bj + r16] =
+                        (double)acc[bi][bj][r];
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const bool ok = diag_compute<true>(sm.d, lane);
+        if (lane == 0) sm.d.ok = ok;
+    }
+    __syncthreads();
+    if (!sm.d.ok) {
+        if (tid == 0) live.status[b] = fd.fail_code;
+        return;
+    }
+    diag_store<float>(sm.d, Ab + (int64_t)(ti * 64) * A.ld + tj * 64, A.ld,
+                      fd.Dinv + b * fd.dstride + (int64_t)ti * 4096, fd.ldet + b * fd.lstride + ti,
+                      tid, 256);
+}
+
+void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
+                               Live live, int nchains, hipStream_t s, FusedDiag<float> fd) {
+    if (ntiles <= 0) return;
+    const long total = (long)ntiles * nchains;
+    hipLaunchKernelGGL(k_chol_update32_t128, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc,
+                       tiles, ntiles, nchains, live, fd);
+}
+
+// Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),
+// j0 <= j <= min(i, jend-1), in 4x4-super-tile blocks (the L2 locality of build_update_tiles);
+// super-tile rows start at i0, columns at j0. Entries without any valid tile are omitted.
+std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi) {
+    std::vector<unsigned> v;
+    auto rowv = [&](int i) { return i < R && !(i >= glo && i < ghi); };
+    const int S = 4;  // super-tiles per block edge (8x8 tiles, as build_update_tiles)
+    const int nr = (R - i0 + 1) / 2, nc = (jend - j0 + 1) / 2;
+    for (int P = 0; P < nr; P += S)
+        for (int Q = 0; Q < nc; Q += S)
+            for (int p = P; p < std::min(P + S, nr); ++p)
+                for (int q = Q; q < std::min(Q + S, nc); ++q) {
+                    const int i = i0 + 2 * p, j = j0 + 2 * q;
+                    const bool rv0 = rowv(i), rv1 = rowv(i + 1);
+                    const bool cv0 = j < jend, cv1 = j + 1 < jend;
+                    bool any = false;
+                    for (int a = 0; a < 2; ++a)
+                        for (int c = 0; c < 2; ++c)
+                            any |= (a ? rv1 : rv0) && (c ? cv1 : cv0) && j + c <= i + a;
+                    if (!any) continue;
+                    v.push_back(((unsigned)i << 18) | ((unsigned)j << 4) | (rv0 ? 1u : 0u) |
+                                (rv1 ? 2u : 0u) | (cv0 ? 4u : 0u) | (cv1 ? 8u : 0u));
+                }
+    return v;
+}
+
 // ------------------------------------------------------------------------------- B in fp32
 // (formed by k_symv_part in the same pass as K b, below)
 

@@ -17,6 +17,7 @@ KERNEL_ISO, KERNEL_ARD, KERNEL_PRECOMPUTED = 0, 1, 2
 EST_IS, EST_PRIORMC, EST_LAPLACE = 0, 1, 2
 STATUS_OK, STATUS_CHOL_K, STATUS_CHOL_B, STATUS_CHOL_C, STATUS_MAXITER = 0, 1, 2, 3, 4
 PROF_GRAM, PROF_CHOL_UPDATE, PROF_UGEMM, PROF_CHOL_UPDATE32, PROF_STATS = 0, 1, 2, 3, 4
+PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER = 5, 6
 
 
 class NativeUnavailableError(RuntimeError):

@@ -118,7 +118,9 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
 #define APM_PROF_CHOL_UPDATE32 3
 #define APM_PROF_STATS 4 /* not a kernel: launches = chains whose mixed-precision Newton solve was
                             rerun in fp64, work = refinement steps launched, total_ms = 0 */
-#define APM_PROF_NKINDS 5
+#define APM_PROF_CHOL_UPDATE32_OUTER 5 /* the rank-64*OUTER launches among CHOL_UPDATE32 */
+#define APM_PROF_CHOL_UPDATE_OUTER 6   /* the rank-64*OUTER launches among CHOL_UPDATE */
+#define APM_PROF_NKINDS 7
 int apm_prof_enable(apm_ctx *ctx, int on);
 /* total device milliseconds and launch count per tracked kernel since the last reset; also the
  * algorithmic work: bytes (GRAM) or flops (CHOL_UPDATE, CHOL_UPDATE32 = the fp32 Newton

@@ -1,8 +1,7 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 120 python -u tools/call_latency.py > gpurun_out/lat.log 2>&1 && \
-APM_SCHED=spin timeout -k 10 120 python -u tools/call_latency.py >> gpurun_out/lat.log 2>&1 && \
-APM_SCHED=yield timeout -k 10 120 python -u tools/call_latency.py >> gpurun_out/lat.log 2>&1 && \
-timeout -k 10 400 python -u bench.py --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/bench.json 2> gpurun_out/bench.err && \
-APM_SCHED=spin timeout -k 10 400 python -u bench.py --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/bench_spin.json 2> gpurun_out/bench_spin.err
+for v in new old new old; do
+  if [ $v = old ]; then export APM_T128=0 APM_LEFT=0 APM_OUTER=4; else unset APM_T128 APM_LEFT APM_OUTER; fi
+  timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-baseline 0 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+  python3 -c "import json; d=json.load(open('gpurun_out/ab_$v.json')); print('$v', round(d['value'],2), round(d['wall_split_s']['theta_call'],2), d['theta_calls_per_transition'])"
+done > gpurun_out/ab.log
