@@ -92,6 +92,12 @@ void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride
                        double* y, int64_t vstride, Live live, int nchains, hipStream_t s);
 void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
                        int64_t vstride, Live live, int nchains, hipStream_t s);
+// the whole solve in one launch (one 1024-thread workgroup per chain), fp64 r -> out (r kept);
+// needs np <= 8192 (trsv32_fused_ok)
+bool trsv32_fused_ok(int np);
+void launch_trsv32_fused(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+                         const double* r, double* out, int64_t vstride, Live live, int nchains,
+                         hipStream_t s);
 // refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
 // acceptance of refinement step `step` on the chains with refining[b] != 0 && status[b] == 0:
 // accepted chains leave the mask; with last = true the others get status = fail_code

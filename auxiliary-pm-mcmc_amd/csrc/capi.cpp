@@ -74,7 +74,8 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     int t128 = 3;
-    bool left_inner = true;  // left-looking updates inside an outer panel (APM_LEFT=0: right)
+    bool left_inner = true;
+    bool trsv_fused = true;  // single-launch TRSV per solve (APM_TRSV_FUSED=0: a launch per block)  // left-looking updates inside an outer panel (APM_LEFT=0: right)
 };
 
 namespace {
@@ -381,9 +382,15 @@ void newton_solve32(apm_ctx* c, int count) {
     chol_range32(c, F, 0, nb, nb + 1, nb, APM_STATUS_CHOL_B, count);  // B32 formed with K b
     launch_row32(F, np, np, r1, vs, lv, count, s);  // y0 = L^-1 rhs (fp32)
     check_launch();
-    for (int J = nb - 1; J >= 0; --J) {
-        launch_trsv_bwd32(F, J, D, ds, r1, c->v.z, vs, lv, count, s);
+    const bool fused_trsv = c->trsv_fused && trsv32_fused_ok(np);
+    if (fused_trsv) {
+        launch_trsv32_fused(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, s);
         check_launch();
+    } else {
+        for (int J = nb - 1; J >= 0; --J) {
+            launch_trsv_bwd32(F, J, D, ds, r1, c->v.z, vs, lv, count, s);
+            check_launch();
+        }
     }
     // fp64 iterative refinement against B = I + W^1/2 K W^1/2, adaptive per chain: a chain
     // leaves after the step its correction passes k_refine_check; one host read of the mask per
@@ -402,13 +409,20 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lr, count, s);       // res
         check_launch();
-        for (int J = 0; J < nb; ++J) {
-            launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lr, count, s);
+        if (fused_trsv) {
+            launch_trsv32_fused(true, F, nb, D, ds, r1, r2, vs, lr, count, s);
             check_launch();
-        }
-        for (int J = nb - 1; J >= 0; --J) {
-            launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lr, count, s);
+            launch_trsv32_fused(false, F, nb, D, ds, r2, r3, vs, lr, count, s);
             check_launch();
+        } else {
+            for (int J = 0; J < nb; ++J) {
+                launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lr, count, s);
+                check_launch();
+            }
+            for (int J = nb - 1; J >= 0; --J) {
+                launch_trsv_bwd32(F, J, D, ds, r2, r3, vs, lr, count, s);
+                check_launch();
+            }
         }
         launch_refine(2, nullptr, nullptr, c->v.z, nullptr, r3, vs, np, lr, count, s);  // x += d
         check_launch();
@@ -654,6 +668,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
+    if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->kind = kind;
     c->n = (int)n;

@@ -655,6 +655,169 @@ __global__ __launch_bounds__(256) void k_trsv_bwd32(MatF A, int J, const float* 
     if (tid < 64) rb[I * 64 + tid] -= part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
 }
 
+// ---------------------------------------------------------------- single-launch TRSV (one WG/chain)
+// The whole solve of one chain in one 1024-thread workgroup, LEFT-looking by 64-row blocks, so no
+// launch per block step and one reduction per step:
+//   FWD  L y = r:    y_J = inv(L_JJ) (r_J - sum_{I<J} L_JI y_I)
+//   BWD  L^T z = r:  z_J = inv(L_JJ)^T (r_J - sum_{I>J} L_IJ^T z_I)
+// Thread t streams the 16-byte pieces (row t/16, columns 4(t%16)..+3) of the tiles of the step
+// (coalesced 256-byte rows), TRF_U tiles of loads in flight, and the first TRF_U tiles (and the
+// inv(L_JJ) piece) of the NEXT step are loaded before this step's reductions, so a step's latency
+// chain (reduce -> barrier -> 64x64 inverse product -> barrier) overlaps the next step's loads.
+// r and the solution so far live in LDS (fp64); partial sums are fp64. FWD row sums reduce over
+// the 16 lanes of a row; BWD column sums over the 64 rows (4 per wave by shuffles, 16 waves through
+// LDS); the inverse product x_J = inv(L_JJ) rj (or its transpose) uses all 1024 threads.
+#define TRF_MAXNP 8192
+#ifndef TRF_U
+#define TRF_U 8  // tiles of loads in flight per thread and step
+#endif
+#define TRF_DP 68  // LDS pitch (floats) of the staged 64x64 inverse
+template <bool FWD>
+__global__ __launch_bounds__(1024) void k_trsv32_fused(MatF A, int nb, const float* Dinv,
+                                                       int64_t dstride, const double* r,
+                                                       double* out, int64_t vstride, Live live) {
+    const int b = blockIdx.x;
+    if (!live32(live, b)) return;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row = t >> 4, cg = t & 15;
+    extern __shared__ double trf_sm[];
+    double* xs = trf_sm;                                      // np: solution so far
+    double* rs = xs + nb * 64;                                // np: right-hand side
+    double* red = rs + nb * 64;                               // 16 x 64 partials
+    double* rj = red + 16 * 64;                               // 64: right-hand side of the step
+    float* DS = reinterpret_cast<float*>(rj + 64);            // 64 x TRF_DP: inv(L_JJ)
+    const float* Lb = A.base + b * A.cstride;
+    const float* Db = Dinv + b * dstride;
+    for (int i = t; i < nb * 64; i += 1024) rs[i] = r[b * vstride + i];
+    // tile piece (step J, tile I) of this thread
+    auto piece = [&](int J, int I) -> const f4_t* {
+        const int64_t o = FWD ? (int64_t)(J * 64 + row) * A.ld + I * 64 + 4 * cg
+                              : (int64_t)(I * 64 + row) * A.ld + J * 64 + 4 * cg;
+        return reinterpret_cast<const f4_t*>(Lb + o);
+    };
+    auto first = [&](int s) { return FWD ? 0 : nb - s; };  // tiles of step s: [first, first + cnt)
+    f4_t pre[TRF_U];
+    f4_t dv = *reinterpret_cast<const f4_t*>(Db + (int64_t)(FWD ? 0 : nb - 1) * 4096 + row * 64 +
+                                             4 * cg);
+    __syncthreads();
+    for (int s = 0; s < nb; ++s) {
+        const int J = FWD ? s : nb - 1 - s;
+        const int cnt = s;  // FWD: I in [0, J); BWD: I in (J, nb) - both s tiles
+        const int i0 = first(s);
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        auto consume = [&](const f4_t& v, int I) {
+            if (FWD) {
+                const double* x = xs + I * 64 + 4 * cg;
+                acc[0] += (double)v[0] * x[0] + (double)v[1] * x[1] + (double)v[2] * x[2] +
+                          (double)v[3] * x[3];
+            } else {
+                const double x = xs[I * 64 + row];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] += (double)v[q] * x;
+            }
+        };
+        // chunk 0 was prefetched during the previous step
+        const int c0 = cnt < TRF_U ? cnt : TRF_U;
+#pragma unroll
+        for (int u = 0; u < TRF_U; ++u)
+            if (u < c0) consume(pre[u], i0 + u);
+        for (int I = i0 + c0; I < i0 + cnt; I += TRF_U) {
+            f4_t v[TRF_U];
+            const int m = min(TRF_U, i0 + cnt - I);
+#pragma unroll
+            for (int u = 0; u < TRF_U; ++u)  // unconditional loads (clamped index): no branches
+                v[u] = *piece(J, min(I + u, i0 + cnt - 1));
+#pragma unroll
+            for (int u = 0; u < TRF_U; ++u)
+                if (u < m) consume(v[u], I + u);
+        }
+        // next step's first chunk and inverse piece, in flight across this step's reductions
+        f4_t dnext = dv;
+        if (s + 1 < nb) {
+            const int Jn = FWD ? s + 1 : nb - 2 - s, in0 = first(s + 1);
+            const int cn = (s + 1) < TRF_U ? (s + 1) : TRF_U;
+#pragma unroll
+            for (int u = 0; u < TRF_U; ++u) pre[u] = *piece(Jn, in0 + min(u, cn - 1));
+            dnext = *reinterpret_cast<const f4_t*>(Db + (int64_t)Jn * 4096 + row * 64 + 4 * cg);
+        }
+        *reinterpret_cast<f4_t*>(DS + row * TRF_DP + 4 * cg) = dv;
+        if (FWD) {  // row sums: 16 lanes per row
+            double sum = acc[0];
+            sum += __shfl_xor(sum, 8, 64);
+            sum += __shfl_xor(sum, 4, 64);
+            sum += __shfl_xor(sum, 2, 64);
+            sum += __shfl_xor(sum, 1, 64);
+            if (cg == 0) rj[row] = rs[J * 64 + row] - sum;
+        } else {  // column sums: the 4 rows of this wave by shuffles, the 16 waves through LDS
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[q] += __shfl_xor(acc[q], 16, 64);
+                acc[q] += __shfl_xor(acc[q], 32, 64);
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) red[w * 64 + 4 * cg + q] = acc[q];
+            }
+        }
+        __syncthreads();
+        if (!FWD) {
+            if (t < 64) {
+                double sum = 0.0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) sum += red[q * 64 + t];
+                rj[t] = rs[J * 64 + t] - sum;
+            }
+            __syncthreads();
+        }
+        {  // x_J[c] = sum_m inv(L_JJ)[c][m] rj[m] (FWD) or inv(L_JJ)[m][c] rj[m] (BWD):
+           // thread (c = t/16, m in 4(t%16)..+3), 16-lane reduction
+            double sum = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = 4 * cg + q;
+                sum += (double)(FWD ? DS[row * TRF_DP + m] : DS[m * TRF_DP + row]) * rj[m];
+            }
+            sum += __shfl_xor(sum, 8, 64);
+            sum += __shfl_xor(sum, 4, 64);
+            sum += __shfl_xor(sum, 2, 64);
+            sum += __shfl_xor(sum, 1, 64);
+            if (cg == 0) {
+                xs[J * 64 + row] = sum;
+                out[b * vstride + J * 64 + row] = sum;
+            }
+        }
+        dv = dnext;
+        __syncthreads();
+    }
+}
+
+static size_t trf_lds_bytes(int nb) {
+    return sizeof(double) * (2 * nb * 64 + 16 * 64 + 64) + sizeof(float) * 64 * TRF_DP;
+}
+
+bool trsv32_fused_ok(int np) { return np <= TRF_MAXNP; }
+
+void launch_trsv32_fused(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+                         const double* r, double* out, int64_t vstride, Live live, int nchains,
+                         hipStream_t s) {
+    const size_t lds = trf_lds_bytes(nb);
+    static bool attr = false;
+    if (!attr) {  // dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP)
+        const int mx = (int)trf_lds_bytes(TRF_MAXNP / 64);
+        (void)hipFuncSetAttribute((const void*)k_trsv32_fused<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipFuncSetAttribute((const void*)k_trsv32_fused<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        attr = true;
+    }
+    if (fwd)
+        hipLaunchKernelGGL(k_trsv32_fused<true>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
+                           dstride, r, out, vstride, live);
+    else
+        hipLaunchKernelGGL(k_trsv32_fused<false>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
+                           dstride, r, out, vstride, live);
+}
+
 void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,
                        double* y, int64_t vstride, Live live, int nchains, hipStream_t s) {
     hipLaunchKernelGGL(k_trsv_fwd32, dim3(nb - J, nchains), dim3(256), 0, s, A, J, Dinv, dstride,

@@ -1,7 +1,7 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for v in new old new old; do
-  if [ $v = old ]; then export APM_T128=0 APM_LEFT=0 APM_OUTER=4; else unset APM_T128 APM_LEFT APM_OUTER; fi
-  timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --cpu-baseline 0 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
-  python3 -c "import json; d=json.load(open('gpurun_out/ab_$v.json')); print('$v', round(d['value'],2), round(d['wall_split_s']['theta_call'],2), d['theta_calls_per_transition'])"
-done > gpurun_out/ab.log
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+tail -3 gpurun_out/gpu_tests.log
+grep -q " passed" gpurun_out/gpu_tests.log && ! grep -q "failed\|error" gpurun_out/gpu_tests.log || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tt_trace -o run -- python3 tools/time_theta.py --batch 64 --reps 2 > gpurun_out/tt_trace.log 2>&1
