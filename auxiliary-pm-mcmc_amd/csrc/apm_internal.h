@@ -171,6 +171,11 @@ void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s);
 void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s);
 void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
                         int nchains, hipStream_t s);
+// out = L^T x (L lower, no reversal)
+void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int np, Live live,
+                    int nchains, hipStream_t s);
+// status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)
+void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s);
 
 // ---- ugemm.hip ------------------------------------------------------------------------------
 struct UPool {

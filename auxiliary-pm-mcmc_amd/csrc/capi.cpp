@@ -75,7 +75,18 @@ struct apm_ctx {
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     int t128 = 3;
     bool left_inner = true;
-    bool trsv_fused = true;  // single-launch TRSV per solve (APM_TRSV_FUSED=0: a launch per block)  // left-looking updates inside an outer panel (APM_LEFT=0: right)
+    bool trsv_fused = true;
+    // chol(K) of the IS theta-call on a low-priority second stream, concurrent with the Newton
+    // iterations (APM_OVERLAP_K=0: after them, on the main stream)
+    bool overlap_k = true;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_gram = nullptr, ev_cholk = nullptr;
+    hipEvent_t ev_feed[4] = {nullptr, nullptr, nullptr, nullptr};
+    int feed_i = 0;
+    int *active2 = nullptr, *status2 = nullptr;
+    // chol(K) is enqueued one outer panel at a time, each released when the main stream enters a
+    // single-workgroup-per-chain TRSV (3/4 of the CUs idle) - see feed_chol_k
+    int cholk_next = -1, cholk_count = 0;  // single-launch TRSV per solve (APM_TRSV_FUSED=0: a launch per block)  // left-looking updates inside an outer panel (APM_LEFT=0: right)
 };
 
 namespace {
@@ -147,6 +158,17 @@ struct ProfScope {
 // ------------------------------------------------------------------------------- building blocks
 Live live_of(apm_ctx* c) { return Live{c->active, c->status}; }
 
+// Where a factorisation runs: stream, liveness, diagonal-inverse / log-det arrays. The main path
+// uses the context stream; chol(K) of the IS theta-call runs concurrently on the low-priority
+// second stream with its own liveness and the upper halves of Dinv / ldet (theta_eval_impl).
+struct Exec {
+    hipStream_t s;
+    Live lv;
+    double* Dinv;
+    double* ldet;
+};
+Exec main_exec(apm_ctx* c) { return Exec{c->stream, live_of(c), c->Dinv, c->ldet}; }
+
 // Two-level right-looking Cholesky over tile columns [k0, k1) of rows < R (tile units), the
 // trailing matrix spanning columns < Cb. Outer panels of OUTER tiles (256 columns) are factored
 // with the 64-wide diag / panel / inner-update steps; the rest of the matrix then receives one
@@ -194,22 +216,23 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
 std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g);
 
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
-                    bool plus, int count, int fuse_k = -1, int fail_code = 0) {
+                    bool plus, int count, int fuse_k = -1, int fail_code = 0,
+                    const Exec* ex = nullptr) {
+    const Exec E = ex ? *ex : main_exec(c);
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
     const auto tl = tile_list(c, i0, R, j0, jend, g);
     if (tl.second <= 0) return;
     FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
-    if (fuse_k >= 0) fd = FusedDiag<double>{1, c->Dinv, c->dstride, c->ldet, c->lstride, fail_code};
+    if (fuse_k >= 0) fd = FusedDiag<double>{1, E.Dinv, c->dstride, E.ldet, c->lstride, fail_code};
     const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0;
-    ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl);
-    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl);
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl, E.s);
+    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
     if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         const auto sl = super_list(c, i0, R, j0, jend, g);
-        launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, live_of(c), count,
-                                c->stream, fd);
+        launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd);
     } else {
-        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, live_of(c), count, c->stream, fd);
+        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, E.lv, count, E.s, fd);
     }
     check_launch();
 }
@@ -223,8 +246,10 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
 void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
-                bool factor_diag = true, int row_start = 0, GapFn gap = no_gap) {
-    const Live lv = live_of(c);
+                bool factor_diag = true, int row_start = 0, GapFn gap = no_gap,
+                const Exec* ex = nullptr) {
+    const Exec E = ex ? *ex : main_exec(c);
+    const Live lv = E.lv;
     const bool fuse = factor_diag && c->fuse_diag && row_start <= k0;
     bool have_diag = false;  // tile (k, k) already factored by the previous update launch
     for (int K = k0; K < k1; K += OUTER) {
@@ -236,38 +261,38 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
             for (int k = K; k < Kend; ++k) {
                 const Gap g = gap(k, c->nb);
                 if (k > K)
-                    tracked_update(c, M, K, k - K, k, R, k, k + 1, g, false, count, k, fail_code);
+                    tracked_update(c, M, K, k - K, k, R, k, k + 1, g, false, count, k, fail_code, &E);
                 else if (!have_diag) {
-                    launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv,
-                                     fail_code, count, c->stream);
+                    launch_chol_diag(M, k, E.Dinv, c->dstride, E.ldet, c->lstride, lv,
+                                     fail_code, count, E.s);
                     check_launch();
                 }
-                launch_chol_panel(M, k, k + 1, R, g.lo, g.hi, c->Dinv, c->dstride, lv, count,
-                                  c->stream);
+                launch_chol_panel(M, k, k + 1, R, g.lo, g.hi, E.Dinv, c->dstride, lv, count,
+                                  E.s);
                 check_launch();
             }
             have_diag = Kend < k1;
             tracked_update(c, M, K, Kend - K, Kend, R, Kend, Cb, gap(Kend - 1, c->nb), false,
-                           count, have_diag ? Kend : -1, fail_code);
+                           count, have_diag ? Kend : -1, fail_code, &E);
             continue;
         }
         for (int k = K; k < Kend; ++k) {
             if (factor_diag && !have_diag) {
-                launch_chol_diag(M, k, c->Dinv, c->dstride, c->ldet, c->lstride, lv, fail_code,
-                                 count, c->stream);
+                launch_chol_diag(M, k, E.Dinv, c->dstride, E.ldet, c->lstride, lv, fail_code,
+                                 count, E.s);
                 check_launch();
             }
             const Gap g = gap(k, c->nb);
-            launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, c->Dinv,
-                              c->dstride, lv, count, c->stream);
+            launch_chol_panel(M, k, std::max(k + 1, row_start), R, g.lo, g.hi, E.Dinv,
+                              c->dstride, lv, count, E.s);
             check_launch();
             have_diag = fuse && k + 1 < Kend;
             tracked_update(c, M, k, 1, std::max(k + 1, row_start), R, k + 1, Kend, g, false,
-                           count, have_diag ? k + 1 : -1, fail_code);
+                           count, have_diag ? k + 1 : -1, fail_code, &E);
         }
         have_diag = fuse && Kend < k1;
         tracked_update(c, M, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb,
-                       gap(Kend - 1, c->nb), false, count, have_diag ? Kend : -1, fail_code);
+                       gap(Kend - 1, c->nb), false, count, have_diag ? Kend : -1, fail_code, &E);
     }
 }
 
@@ -371,6 +396,8 @@ void u_eval_device(apm_ctx* c, int count) {
 // Newton loop of laplace_approximation over the live chains; returns host n_iter per chain.
 // B x = W^1/2 K b with the fp32 factor (its forward solve is the appended row np) and n_refine
 // steps of fp64 iterative refinement; x -> v.z (chol32.hip)
+void feed_chol_k(apm_ctx* c);
+
 void newton_solve32(apm_ctx* c, int count) {
     const Live lv = live_of(c);
     hipStream_t s = c->stream;
@@ -384,6 +411,7 @@ void newton_solve32(apm_ctx* c, int count) {
     check_launch();
     const bool fused_trsv = c->trsv_fused && trsv32_fused_ok(np);
     if (fused_trsv) {
+        feed_chol_k(c);
         launch_trsv32_fused(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, s);
         check_launch();
     } else {
@@ -410,8 +438,10 @@ void newton_solve32(apm_ctx* c, int count) {
         launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lr, count, s);       // res
         check_launch();
         if (fused_trsv) {
+            feed_chol_k(c);
             launch_trsv32_fused(true, F, nb, D, ds, r1, r2, vs, lr, count, s);
             check_launch();
+            feed_chol_k(c);
             launch_trsv32_fused(false, F, nb, D, ds, r2, r3, vs, lr, count, s);
             check_launch();
         } else {
@@ -545,21 +575,69 @@ void augmented(apm_ctx* c, int count, bool factor_C) {
 // Posterior-covariance factor through chol(K) (postcov.hip): 4N^3/3 flops instead of the
 // augmented 7N^3/3. Leaves chol(C) J in rows [np, 2np) x cols [0, np) of A, g in v.Kb and
 // log|B| = log|M| in ldet[0..nb).
-void post_cov_lk(apm_ctx* c, int count) {
+MatB bl_of(apm_ctx* c) { return MatB{c->A.base + (int64_t)c->np * c->A.ld, c->A.ld, c->A.cstride}; }
+
+// chol(K) into the bottom-left block BL of the work matrix for the concurrent path: own stream
+// (ex.s), liveness (active2 / status2, so that Newton convergence does not mask it) and the upper
+// halves of Dinv / ldet (the Newton factorisation uses the lower halves and the top rows of A).
+// chol_k_begin copies K and factors the first outer panel; each feed_chol_k call releases the
+// next outer panel (panel + its trailing update) behind an event of the main stream.
+Exec k_exec(apm_ctx* c, hipStream_t s);
+void chol_k_panel(apm_ctx* c, const Exec& ex) {
+    const int K = c->cholk_next;
+    if (K < 0 || K >= c->nb) return;
+    chol_range(c, bl_of(c), K, std::min(K + OUTER, c->nb), c->nb, c->nb, APM_STATUS_CHOL_K,
+               c->cholk_count, true, 0, no_gap, &ex);
+    c->cholk_next = K + OUTER;
+}
+void chol_k_begin(apm_ctx* c, int count, const Exec& ex) {
+    HIPC(hipMemsetD32Async(c->active2, 1, count, ex.s));
+    HIPC(hipMemsetAsync(c->status2, 0, sizeof(int) * count, ex.s));
+    launch_copy_lower(c->K, bl_of(c), c->np, ex.lv, count, ex.s);
+    check_launch();
+    c->cholk_next = 0;
+    c->cholk_count = count;
+    chol_k_panel(c, ex);
+}
+void feed_chol_k(apm_ctx* c) {
+    if (c->cholk_next < 0 || c->cholk_next >= c->nb) return;
+    hipEvent_t e = c->ev_feed[c->feed_i++ & 3];
+    HIPC(hipEventRecord(e, c->stream));
+    HIPC(hipStreamWaitEvent(c->stream2, e, 0));
+    chol_k_panel(c, k_exec(c, c->stream2));
+}
+// all of chol(K) on one stream (the rerun after an fp64 Newton fallback)
+void chol_k_into_bl(apm_ctx* c, int count, const Exec& ex) {
+    chol_k_begin(c, count, ex);
+    while (c->cholk_next >= 0 && c->cholk_next < c->nb) chol_k_panel(c, ex);
+    c->cholk_next = -1;
+}
+
+Exec k_exec(apm_ctx* c, hipStream_t s) {
+    return Exec{s, Live{c->active2, c->status2}, c->Dinv + (int64_t)c->nb * 4096, c->ldet + c->nb};
+}
+
+// L_K ready in BL (chol_k_into_bl); h = L_K^-1 f_post = L_K^T a because f_post = K a
+void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     const Live lv = live_of(c);
     hipStream_t s = c->stream;
     HIPC(hipMemsetD32Async(c->active, 1, count, s));
     const int nb = c->nb, np = c->np;
     const int64_t vs = c->v.vstride;
     MatB TL = c->A;
-    MatB BL{c->A.base + (int64_t)np * c->A.ld, c->A.ld, c->A.cstride};
-    launch_copy_lower(c->K, BL, np, lv, count, s);
-    check_launch();
-    launch_set_rhs(c->A, 2 * (int64_t)np, np, c->v.f, vs, lv, count, s);  // f_post under K
-    check_launch();
-    chol_range(c, BL, 0, nb, nb + 1, nb, APM_STATUS_CHOL_K, count);       // L_K, h = L_K^-1 f
-    launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
-    check_launch();
+    MatB BL = bl_of(c);
+    if (have_lk) {
+        launch_trmv_lt(BL, c->v.a, c->v.z, vs, np, lv, count, s);          // h = L_K^T a -> z
+        check_launch();
+    } else {
+        launch_copy_lower(c->K, BL, np, lv, count, s);
+        check_launch();
+        launch_set_rhs(c->A, 2 * (int64_t)np, np, c->v.f, vs, lv, count, s);  // f_post under K
+        check_launch();
+        chol_range(c, BL, 0, nb, nb + 1, nb, APM_STATUS_CHOL_K, count);       // L_K, h = L_K^-1 f
+        launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
+        check_launch();
+    }
     launch_form_y2(BL, TL, np, c->v.Ws, vs, np, lv, count, s);           // Y2 = J Z^T J
     check_launch();
     launch_reverse_cols(BL, np, lv, count, s);                           // Y = L_K J
@@ -598,10 +676,29 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         check_launch();
         u_eval_device(c, count);
     } else {
+        // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
+        const bool ov = est == APM_EST_IS && !c->postcov_aug && c->mixed && c->overlap_k;
+        if (ov) {
+            HIPC(hipEventRecord(c->ev_gram, c->stream));
+            HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
+            chol_k_begin(c, count, k_exec(c, c->stream2));
+        }
+        const int64_t reruns = c->n_fp64_rerun;
         if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself
             newton(c, count, st_h, false);
         else
             newton_is(c, count, st_h);
+        if (ov) {
+            while (c->cholk_next >= 0 && c->cholk_next < c->nb)  // what the TRSVs did not take
+                chol_k_panel(c, k_exec(c, c->stream2));
+            c->cholk_next = -1;
+            HIPC(hipEventRecord(c->ev_cholk, c->stream2));
+            HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
+            if (c->n_fp64_rerun != reruns)  // the fp64 Newton rerun used rows of BL: redo L_K
+                chol_k_into_bl(c, count, k_exec(c, c->stream));
+            launch_merge_status(c->status, c->status2, APM_STATUS_CHOL_K, count, c->stream);
+            check_launch();
+        }
         if (est == APM_EST_LAPLACE) {
             launch_laplace_lml(c->v, c->y, c->n, c->ldet, c->lstride, c->nb, c->out, lv, count,
                                c->stream);
@@ -612,7 +709,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                 augmented(c, count, true);
                 mode = 0;
             } else {
-                post_cov_lk(c, count);
+                post_cov_lk(c, count, ov);
             }
             launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, mode,
                               c->n, c->np, lv, count, c->stream);
@@ -669,7 +766,16 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
-    HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
+    {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
+        int least = 0, greatest = 0;
+        HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPC(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+        HIPC(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, least));
+        HIPC(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&c->ev_cholk, hipEventDisableTiming));
+        for (hipEvent_t& e : c->ev_feed) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     c->kind = kind;
     c->n = (int)n;
     c->d = (int)d;
@@ -719,6 +825,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->status = dalloc<int>(c, B);
     c->n_iter = dalloc<int>(c, B);
     c->refining = dalloc<int>(c, B);
+    c->active2 = dalloc<int>(c, B);
+    c->status2 = dalloc<int>(c, B);
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, B);
     c->d_ubufs = dalloc<int64_t>(c, B);
@@ -743,7 +851,13 @@ void free_ctx(apm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->ev_gram) (void)hipEventDestroy(c->ev_gram);
+    if (c->ev_cholk) (void)hipEventDestroy(c->ev_cholk);
+    for (hipEvent_t e : c->ev_feed)
+        if (e) (void)hipEventDestroy(e);
     delete c;
 }
 

@@ -128,11 +128,13 @@ void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s
     hipLaunchKernelGGL(k_identity_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, M, live);
 }
 
-// g = J L'^T J h: g[np-1-c] = sum_{r >= c} L'[r][c] h[np-1-r]; one workgroup per 64-column block,
-// each wave strides over rows (512-byte coalesced row segments), waves reduced through LDS.
-__global__ __launch_bounds__(256) void k_trmv_lt_rev(MatB L, const double* __restrict__ h,
-                                                     double* __restrict__ g, int64_t vstride,
-                                                     int np, Live live) {
+// g = J L'^T J h: g[np-1-c] = sum_{r >= c} L'[r][c] h[np-1-r] (REV), or out[c] = sum_{r >= c}
+// L[r][c] x[r] (h = L_K^T a); one workgroup per 64-column block, each wave strides over rows
+// (512-byte coalesced row segments), waves reduced through LDS.
+template <bool REV>
+__global__ __launch_bounds__(256) void k_trmv_lt(MatB L, const double* __restrict__ h,
+                                                 double* __restrict__ g, int64_t vstride, int np,
+                                                 Live live) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
     const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -141,15 +143,33 @@ __global__ __launch_bounds__(256) void k_trmv_lt_rev(MatB L, const double* __res
     const double* hb = h + b * vstride;
     double s = 0.0;
     for (int r = cb * 64 + w; r < np; r += 4)
-        if (r >= c) s += Lb[(int64_t)r * L.ld + c] * hb[np - 1 - r];
+        if (r >= c) s += Lb[(int64_t)r * L.ld + c] * hb[REV ? np - 1 - r : r];
     __shared__ double red[4][64];
     red[w][lane] = s;
     __syncthreads();
-    if (w == 0) g[b * vstride + np - 1 - c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (w == 0)
+        g[b * vstride + (REV ? np - 1 - c : c)] =
+            red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
 void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
                         int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_trmv_lt_rev, dim3(np / 64, nchains), dim3(256), 0, s, L, h, g, vstride, np,
-                       live);
+    hipLaunchKernelGGL(k_trmv_lt<true>, dim3(np / 64, nchains), dim3(256), 0, s, L, h, g, vstride,
+                       np, live);
+}
+
+void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int np, Live live,
+                    int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_trmv_lt<false>, dim3(np / 64, nchains), dim3(256), 0, s, L, x, out,
+                       vstride, np, live);
+}
+
+__global__ void k_merge_status(int* status, const int* other, int code, int nchains) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nchains && other[b] != 0) status[b] = code;
+}
+
+void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s) {
+    hipLaunchKernelGGL(k_merge_status, dim3((nchains + 255) / 256), dim3(256), 0, s, status, other,
+                       code, nchains);
 }
