@@ -34,16 +34,6 @@ __device__ __forceinline__ double log_ndtr_d(double z) {
     return log1p(-0.5 * erfc(z * rs2));
 }
 
-// fp32, branch-free (no divergence inside a wave): one erfcx for both signs,
-//   t = |z|/sqrt2, e = erfcx(t):  z < 0 : log(e/2) - t^2;   z >= 0 : log1p(-e exp(-t^2) / 2)
-__device__ __forceinline__ float log_ndtr_fast(float z) {
-    const float t = fabsf(z) * 0.70710678118654752440f;
-    const float e = erfcxf(t);
-    const float neg = __logf(0.5f * e) - t * t;
-    const float pos = log1pf(-0.5f * e * __expf(-t * t));
-    return z < 0.0f ? neg : pos;
-}
-
 __device__ __forceinline__ float log_ndtr_f(float z) {
     const float rs2 = 0.70710678118654752440f;
     if (z < 0.0f) return __logf(0.5f * erfcxf(-z * rs2)) - 0.5f * z * z;

@@ -179,7 +179,7 @@ void launch_merge_status(int* status, const int* other, int code, int nchains, h
 
 // ---- ugemm.hip ------------------------------------------------------------------------------
 struct UPool {
-    float* base;        // each buffer: sp x np fp32 (sample-major: (i, s) at s*np + i), zero padded
+    float* base;        // each buffer: np x sp fp32, ld = sp, zero padded
     int64_t stride;
     int sp;
 };

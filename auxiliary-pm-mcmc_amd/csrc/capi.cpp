@@ -944,7 +944,7 @@ int apm_u_download(apm_ctx* c, int64_t ubuf, double* U, int64_t ldu) {
                             hipMemcpyDeviceToHost, c->stream));
         sync(c);
         for (int i = 0; i < c->n; ++i)
-            for (int s = 0; s < c->S; ++s) U[(int64_t)i * ldu + s] = h[(size_t)s * c->np + i];
+            for (int s = 0; s < c->S; ++s) U[(int64_t)i * ldu + s] = h[(size_t)i * c->sp + s];
     } catch (const HipError& e) {
         return fail(c, APM_E_HIP, e.msg);
     }

@@ -3,6 +3,7 @@
 There is deliberately no CPU fallback: if the library is missing or no HIP device is visible,
 every estimator / kernel entry point raises :class:`NativeUnavailableError`.
 """
+import collections
 import ctypes
 import os
 import threading
@@ -207,6 +208,8 @@ class Context(object):
                               (lib.apm_global_error() or b'').decode(errors='replace'))
         self.slots = _Pool(int(n_slots))
         self.ubufs = _Pool(int(n_ubufs))
+        # calls per batch size (bench.py reports the timed region's; launch shapes depend on it)
+        self.batch_hist = {'u': collections.Counter(), 'theta': collections.Counter()}
         self.theta_len = int(lib.apm_theta_len(self._h))
         self.padded_n = int(lib.apm_padded_n(self._h))
 
@@ -256,6 +259,7 @@ class Context(object):
     def theta_eval(self, est, thetas, ubufs=None, slots=None):
         th = np.atleast_2d(_f64(thetas))
         count = th.shape[0]
+        self.batch_hist['theta'][count] += 1
         if th.shape[1] < self.theta_len:
             raise IndexError('Out of bounds on buffer access (axis 0)')
         out = np.full(count, np.nan)
@@ -278,6 +282,7 @@ class Context(object):
 
     def u_eval(self, slots, ubufs):
         sl = np.ascontiguousarray(slots, dtype=np.int64)
+        self.batch_hist['u'][sl.shape[0]] += 1
         ub = np.ascontiguousarray(ubufs, dtype=np.int64)
         out = np.full(sl.shape[0], np.nan)
         st = np.zeros(sl.shape[0], dtype=np.int32)

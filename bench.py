@@ -206,6 +206,8 @@ def main():
     device_sync()  # first torch touch outside the timed region
     mark = lambda: ctx.prof_marker(1)  # noqa: E731  timed-region bracket (tools/prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
+    for h in ctx.batch_hist.values():
+        h.clear()
     for k in smp.wall:
         smp.wall[k] = 0.
     res = {}
@@ -322,6 +324,7 @@ def main():
         'newton_refinement_steps': int(dist.sum(n_refine)),
         'newton_fp64_reruns': int(dist.sum(n_rerun)),
         'wall_split_s': dict(smp.wall, host_sampler=elapsed - sum(smp.wall.values())),
+        'calls_by_batch_size': {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()},
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)

@@ -13,6 +13,7 @@ T=$(find $O/trace -name '*kernel_trace.csv' | head -1)
 F=$(find $O/fetch -name '*counter_collection.csv' | head -1)
 W=$(find $O/write -name '*counter_collection.csv' | head -1)
 python3 tools/prof_window.py "$T" --fetch "$F" --write "$W" --out $O/window.json > $O/window.txt
+python3 tools/idle_gaps.py "$T" > $O/idle_gaps.txt
 find $O -name '*kernel_trace.csv' -delete
 find $O -name '*counter_collection.csv' -delete
 du -sh $O
