@@ -76,6 +76,8 @@ struct apm_ctx {
     int t128 = 3;
     bool left_inner = true;
     bool trsv_fused = true;
+    bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
+    bool h3_now = false;  // fp16x3 allowed for the current theta-call (range check on theta_0)
     // chol(K) of the IS theta-call on a low-priority second stream, concurrent with the Newton
     // iterations (APM_OVERLAP_K=0: after them, on the main stream)
     bool overlap_k = true;
@@ -329,7 +331,7 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     if ((c->t128 & 1) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0});
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  fd);
+                                  fd, c->h3_now ? c->nb : 0);
     } else {
         launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd);
     }
@@ -767,6 +769,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
+    if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1019,6 +1022,9 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
             for (int p = 0; p < c->P; ++p) th[b * c->P + p] = thetas[b * ldt + p];
         HIPC(hipMemcpyAsync(c->theta, th.data(), sizeof(double) * th.size(), hipMemcpyHostToDevice,
                             c->stream));
+        // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip)
+        c->h3_now = c->h3;
+        for (int64_t b = 0; b < count; ++b) c->h3_now &= th[b * c->P] < 19.0;
         if (est != APM_EST_LAPLACE) {
             HIPC(hipMemcpyAsync(c->d_slots, slots, sizeof(int64_t) * count, hipMemcpyHostToDevice,
                                 c->stream));
@@ -1049,6 +1055,9 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
                     (i < c->n && j < c->n) ? K[(int64_t)i * ldk + j] : (i == j ? 1.0 : 0.0);
         HIPC(hipMemcpyAsync(c->K.base, Kp.data(), sizeof(double) * Kp.size(),
                             hipMemcpyHostToDevice, c->stream));
+        double kmax = 0.0;
+        for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
+        c->h3_now = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
         HIPC(hipMemcpyAsync(c->d_slots, &slot, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
         HIPC(hipMemcpyAsync(c->d_ubufs, &ubuf, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);
