@@ -74,7 +74,8 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
                          int64_t dstride, Live live, int nchains, hipStream_t s);
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
-                          FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0});
+                          FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
+                          int hlim = 0);
 // the same update with one 128x128 super-tile per workgroup (tiles from build_update_supertiles);
 // hlim > 0: fp16x3 operands (chol32.hip) for super-tiles whose rows lie below row tile hlim
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,

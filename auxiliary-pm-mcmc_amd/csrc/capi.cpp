@@ -333,7 +333,8 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
                                   fd, c->h3_now ? c->nb : 0);
     } else {
-        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd);
+        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd,
+                             c->h3_now ? c->nb : 0);
     }
     check_launch();
 }

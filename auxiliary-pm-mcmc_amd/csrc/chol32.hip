@@ -23,10 +23,32 @@
 
 #define KS32 32          // slice depth (floats) of the LDS-staged tile GEMM
 #define LP32 (KS32 + 2)  // pitch 34 floats: fragment reads (16 rows x 4 k) hit 32 distinct banks
+// fp16x3 operands (see k_chol_update32_t128): hi and lo halves of a 32-deep slice, rows padded to
+// 40 halves (80 B: the 16-byte fragment reads of 8 row-consecutive lanes hit 8 distinct 16-byte
+// bank groups)
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+#define LPH 40
 struct GemmSmem32 {
-    float a[2][64][LP32];
-    float b[2][64][LP32];
+    union {
+        struct {
+            float a[2][64][LP32];
+            float b[2][64][LP32];
+        };
+        struct {
+            _Float16 ah[2][64][LPH], al[2][64][LPH];
+            _Float16 bh[2][64][LPH], bl[2][64][LPH];
+        };
+    };
 };
+__device__ __forceinline__ void split_h3(const f4_t& v, h4_t& hi, h4_t& lo) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const _Float16 x = (_Float16)v[e];
+        hi[e] = x;
+        lo[e] = (_Float16)(v[e] - (float)x);
+    }
+}
 // v_mfma_f32_16x16x4_f32: A lane l holds A[l&15][k=l>>4], B holds B[k=l>>4][l&15];
 // D reg r of lane l is (row 4*(l>>4) + r, col l&15)  (cdna_hip_programming.md §3)
 #define F32_CROW(l, r) (4 * ((l) >> 4) + (r))
@@ -61,8 +83,9 @@ __device__ __forceinline__ void tile32_store(const f4_t (&acc)[2][2], float* T, 
 
 // acc += (NEG ? -1 : 1) * A[64 x depth] * B[64 x depth]^T (+ C if given): the fp32 twin of
 // chol.hip's tile_gemm_nt (two slices of loads in flight, double-buffered LDS, one barrier per
-// slice, the old tile loaded behind the first slices and added at the end).
-template <bool NEG>
+// slice, the old tile loaded behind the first slices and added at the end). H3: fp16x3 operands
+// on v_mfma_f32_16x16x32_f16 (as k_chol_update32_t128).
+template <bool NEG, bool H3 = false>
 __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* __restrict__ A,
                                                int64_t lda, const float* __restrict__ B,
                                                int64_t ldb, int depth, GemmSmem32& sm,
@@ -87,6 +110,19 @@ __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* _
         }
     };
     auto sstore = [&](int buf, const f4_t (&ra)[PPT], const f4_t (&rb)[PPT]) {
+        if constexpr (H3) {
+#pragma unroll
+            for (int h = 0; h < PPT; ++h) {
+                h4_t hi, lo;
+                split_h3(NEG ? -ra[h] : ra[h], hi, lo);
+                *reinterpret_cast<h4_t*>(&sm.ah[buf][prow[h]][pcol[h]]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.al[buf][prow[h]][pcol[h]]) = lo;
+                split_h3(rb[h], hi, lo);
+                *reinterpret_cast<h4_t*>(&sm.bh[buf][prow[h]][pcol[h]]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.bl[buf][prow[h]][pcol[h]]) = lo;
+            }
+            return;
+        }
 #pragma unroll
         for (int h = 0; h < PPT; ++h)
 #pragma unroll
@@ -96,6 +132,25 @@ __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* _
             }
     };
     auto compute = [&](int cur) {
+        if constexpr (H3) {  // lane (r16, kq): k = 8kq .. 8kq+7 of the slice
+            h8_t ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                ah[x] = *reinterpret_cast<const h8_t*>(&sm.ah[cur][32 * wr + 16 * x + r16][8 * kq]);
+                al[x] = *reinterpret_cast<const h8_t*>(&sm.al[cur][32 * wr + 16 * x + r16][8 * kq]);
+                bh[x] = *reinterpret_cast<const h8_t*>(&sm.bh[cur][32 * wc + 16 * x + r16][8 * kq]);
+                bl[x] = *reinterpret_cast<const h8_t*>(&sm.bl[cur][32 * wc + 16 * x + r16][8 * kq]);
+            }
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj) {
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < KS32 / 4; ++t) {
             float a[2], b[2];
@@ -181,7 +236,7 @@ __device__ __forceinline__ long xcd_remap32(long L, long total) {
 __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
                                                        const unsigned* __restrict__ tiles,
                                                        int ntiles, int nchains, Live live,
-                                                       FusedDiag<float> fd) {
+                                                       FusedDiag<float> fd, int hlim) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -209,8 +264,14 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-    tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
-                         Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm.g, Aij, A.ld);
+    if (i < hlim)  // fp16x3 below the appended right-hand-side row tile (k_chol_update32_t128)
+        tile_gemm_nt32<true, true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
+                                   Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm.g,
+                                   Aij, A.ld);
+    else
+        tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
+                             Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm.g, Aij,
+                             A.ld);
     if (!fused) {
         tile32_store(acc, Aij, A.ld, wr, wc, lane);
         return;
@@ -238,11 +299,11 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
 }
 
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                          int nchains, hipStream_t s, FusedDiag<float> fd) {
+                          int nchains, hipStream_t s, FusedDiag<float> fd, int hlim) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, live, fd);
+                       ntiles, nchains, live, fd, hlim);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -256,16 +317,11 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 // out-of-range reads) and their results are dropped.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
-typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
-typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 #define KS128 32
 struct __attribute__((aligned(16))) GemmSmem128 {  // fp32 operands, LDS-DMA image
     float a[2][128][KS128];
     float b[2][128][KS128];
 };
-// fp16x3 operands: hi and lo halves of a 32-deep slice, rows padded to 40 halves (80 B: the
-// 16-byte fragment reads of 8 row-consecutive lanes hit 8 distinct 16-byte bank groups)
-#define LPH 40
 struct __attribute__((aligned(16))) GemmSmemH3 {
     _Float16 ah[2][128][LPH], al[2][128][LPH];
     _Float16 bh[2][128][LPH], bl[2][128][LPH];
