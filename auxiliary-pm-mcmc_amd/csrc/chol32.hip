@@ -629,11 +629,14 @@ void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Li
 }
 
 // ------------------------------------------------------------------------------- K x (symmetric)
-// y = K x reading only K's lower tiles (half the bytes of a full GEMV): workgroup (ti, tj) stages
-// tile K_ij in LDS and writes the partial products K_ij x_j (row sums) to part[ti][tj] and, off
-// the diagonal, K_ij^T x_i (column sums) to part[tj][ti]; k_symv_reduce adds the nb partials of
-// every row in a fixed order (deterministic, no atomics). With `Bf` set, the same pass also
-// writes the fp32 Newton matrix tile I + W^1/2 K W^1/2 (fusing k_form_B32 into the x = b pass).
+// y = K x reading only K's lower tiles (half the bytes of a full GEMV): workgroup (ti, tj) reads
+// tile K_ij straight into registers - thread t holds rows 4(t/16) .. +3, columns 4(t%16) .. +3
+// (8 x 16-byte loads, 512-byte rows per 16 lanes, all issued at once) - and writes the partial
+// products K_ij x_j (row sums: 16-lane shuffles) to part[ti][tj] and, off the diagonal, K_ij^T x_i
+// (column sums: shuffles across the 4 row groups of a wave, then the 4 waves through LDS) to
+// part[tj][ti]; k_symv_reduce adds the nb partials of every row in a fixed order (deterministic,
+// no atomics). With `Bf` set, the same pass also writes the fp32 Newton matrix tile
+// I + W^1/2 K W^1/2 (fusing k_form_B32 into the x = b pass).
 __global__ __launch_bounds__(256) void k_symv_part(MatB K, const double* __restrict__ x,
                                                    int64_t xstride, double* __restrict__ part,
                                                    int64_t pstride, int nb, MatF Bf,
@@ -646,44 +649,77 @@ __global__ __launch_bounds__(256) void k_symv_part(MatB K, const double* __restr
     while (ti * (ti + 1) / 2 > t) --ti;
     while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
     const int tj = t - ti * (ti + 1) / 2;
-    __shared__ double T[64][65];
-    __shared__ double xi[64], xj[64];
-    const int tid = threadIdx.x;
-    const double* Kt = K.base + b * K.cstride + (int64_t)(ti * 64) * K.ld + tj * 64;
-    const double* wb = Ws ? Ws + b * wstride : nullptr;
-    float* Fb = Bf.base ? Bf.base + b * Bf.cstride + (int64_t)(ti * 64) * Bf.ld + tj * 64 : nullptr;
-#pragma unroll 4
-    for (int e = tid; e < 2048; e += 256) {  // 16-byte loads, rows of 512 B
-        const int r = e >> 5, c2 = (e & 31) * 2;
-        const d2_t v = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld + c2);
-        T[r][c2] = v.x;
-        T[r][c2 + 1] = v.y;
-        if (Fb) {
-            const int gr = ti * 64 + r, gc = tj * 64 + c2;
-            const double wr_ = wb[gr];
-            float2 o;
-            o.x = (float)((gr == gc ? 1.0 : 0.0) + (wr_ * v.x) * wb[gc]);
-            o.y = (float)((gr == gc + 1 ? 1.0 : 0.0) + (wr_ * v.y) * wb[gc + 1]);
-            *reinterpret_cast<float2*>(Fb + (int64_t)r * Bf.ld + c2) = o;
-        }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rg = tid >> 4, cg = tid & 15;  // rows 4rg .. 4rg+3, columns 4cg .. 4cg+3
+    const double* Kt = K.base + b * K.cstride + (int64_t)(ti * 64 + 4 * rg) * K.ld + tj * 64 + 4 * cg;
+    d2_t v[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[r][0] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld);
+        v[r][1] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld + 2);
     }
     const double* xb = x + b * xstride;
-    if (tid < 64) xj[tid] = xb[tj * 64 + tid];
-    else if (tid < 128) xi[tid - 64] = xb[ti * 64 + tid - 64];
-    __syncthreads();
-    double* pb = part + b * pstride;
-    if (tid < 64) {  // row sums: part[ti][tj][r]
-        double s = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < 64; ++c) s = fma(T[tid][c], xj[c], s);
-        pb[((int64_t)ti * nb + tj) * 64 + tid] = s;
-    } else if (tid < 128 && ti != tj) {  // column sums: part[tj][ti][c]
-        const int c = tid - 64;
-        double s = 0.0;
-#pragma unroll 8
-        for (int r = 0; r < 64; ++r) s = fma(T[r][c], xi[r], s);
-        pb[((int64_t)tj * nb + ti) * 64 + c] = s;
+    const d2_t xj0 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg);
+    const d2_t xj1 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg + 2);
+    const d2_t xi0 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg);
+    const d2_t xi1 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg + 2);
+    const double xjv[4] = {xj0.x, xj0.y, xj1.x, xj1.y}, xiv[4] = {xi0.x, xi0.y, xi1.x, xi1.y};
+    if (Bf.base) {
+        const double* wb = Ws + b * wstride;
+        float* Fb = Bf.base + b * Bf.cstride + (int64_t)(ti * 64 + 4 * rg) * Bf.ld + tj * 64 + 4 * cg;
+        const int gr0 = ti * 64 + 4 * rg, gc0 = tj * 64 + 4 * cg;
+        const d2_t wc0 = *reinterpret_cast<const d2_t*>(wb + gc0);
+        const d2_t wc1 = *reinterpret_cast<const d2_t*>(wb + gc0 + 2);
+        const double wcv[4] = {wc0.x, wc0.y, wc1.x, wc1.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double wr_ = wb[gr0 + r];
+            const double kv[4] = {v[r][0].x, v[r][0].y, v[r][1].x, v[r][1].y};
+            f4_t o;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                o[c] = (float)((gr0 + r == gc0 + c ? 1.0 : 0.0) + (wr_ * kv[c]) * wcv[c]);
+            *reinterpret_cast<f4_t*>(Fb + (int64_t)r * Bf.ld) = o;
+        }
     }
+    double* pb = part + b * pstride;
+    // row sums over this thread's 4 columns, then over the 16 lanes of the row group
+    double rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double sr = v[r][0].x * xjv[0];
+        sr = fma(v[r][0].y, xjv[1], sr);
+        sr = fma(v[r][1].x, xjv[2], sr);
+        sr = fma(v[r][1].y, xjv[3], sr);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
+        rs[r] = sr;
+    }
+    if (cg < 4) pb[((int64_t)ti * nb + tj) * 64 + 4 * rg + cg] = rs[cg];
+    if (ti == tj) return;  // uniform per workgroup
+    // column sums over this thread's 4 rows, then over the 4 row groups of the wave and 4 waves
+    __shared__ double cs[4][64];
+    double csum[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double kc0 = c < 2 ? (c == 0 ? v[0][0].x : v[0][0].y) : (c == 2 ? v[0][1].x : v[0][1].y);
+        const double kc1 = c < 2 ? (c == 0 ? v[1][0].x : v[1][0].y) : (c == 2 ? v[1][1].x : v[1][1].y);
+        const double kc2 = c < 2 ? (c == 0 ? v[2][0].x : v[2][0].y) : (c == 2 ? v[2][1].x : v[2][1].y);
+        const double kc3 = c < 2 ? (c == 0 ? v[3][0].x : v[3][0].y) : (c == 2 ? v[3][1].x : v[3][1].y);
+        double sc = kc0 * xiv[0];
+        sc = fma(kc1, xiv[1], sc);
+        sc = fma(kc2, xiv[2], sc);
+        sc = fma(kc3, xiv[3], sc);
+        sc += __shfl_xor(sc, 16, 64);
+        sc += __shfl_xor(sc, 32, 64);
+        csum[c] = sc;
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cs[w][4 * lane + c] = csum[c];
+    }
+    __syncthreads();
+    if (tid < 64) pb[((int64_t)tj * nb + ti) * 64 + tid] = cs[0][tid] + cs[1][tid] + cs[2][tid] + cs[3][tid];
 }
 
 // y[i] = sum_tj part[i/64][tj][i%64]; with Bf: also the Newton right-hand-side block of the fp32
