@@ -98,6 +98,11 @@ void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double
 // the whole solve in one launch (one 1024-thread workgroup per chain), fp64 r -> out (r kept);
 // needs np <= 8192 (trsv32_fused_ok)
 bool trsv32_fused_ok(int np);
+// the same solve over TRM_G workgroups per chain (k_trsv32_mw; NaN-fills `out` first)
+bool trsv32_mw_ok(int np);
+void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+                      const double* r, double* out, int64_t vstride, Live live, int nchains,
+                      int fail_code, hipStream_t s);
 void launch_trsv32_fused(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                          const double* r, double* out, int64_t vstride, Live live, int nchains,
                          hipStream_t s);

@@ -76,6 +76,7 @@ struct apm_ctx {
     int t128 = 3;
     bool left_inner = true;
     bool trsv_fused = true;
+    bool trsv_mw = true;  // APM_TRSV_MW=0: one workgroup per chain (k_trsv32_fused)
     bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
     bool h3_now = false;  // fp16x3 allowed for the current theta-call (range check on theta_0)
     // chol(K) of the IS theta-call on a low-priority second stream, concurrent with the Newton
@@ -178,6 +179,7 @@ Exec main_exec(apm_ctx* c) { return Exec{c->stream, live_of(c), c->Dinv, c->ldet
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
 static int OUTER = 8;  // tiles per outer panel (APM_OUTER overrides, development knob)
+static int OUTER32 = 8;  // the same for the Newton factorisation (APM_OUTER32)
 
 // Row tiles [lo, hi) known to be zero in panel column k (skipped by panel and update).
 struct Gap {
@@ -345,8 +347,8 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
-    for (int K = k0; K < k1; K += OUTER) {
-        const int Kend = std::min(K + OUTER, k1);
+    for (int K = k0; K < k1; K += OUTER32) {
+        const int Kend = std::min(K + OUTER32, k1);
         if (c->fuse_diag && c->left_inner) {  // left-looking inside the panel (chol_range)
             for (int k = K; k < Kend; ++k) {
                 if (k > K)
@@ -415,7 +417,10 @@ void newton_solve32(apm_ctx* c, int count) {
     const bool fused_trsv = c->trsv_fused && trsv32_fused_ok(np);
     if (fused_trsv) {
         feed_chol_k(c);
-        launch_trsv32_fused(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, s);
+        if (c->trsv_mw)
+            launch_trsv32_mw(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, APM_STATUS_CHOL_B, s);
+        else
+            launch_trsv32_fused(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, s);
         check_launch();
     } else {
         for (int J = nb - 1; J >= 0; --J) {
@@ -442,10 +447,16 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         if (fused_trsv) {
             feed_chol_k(c);
-            launch_trsv32_fused(true, F, nb, D, ds, r1, r2, vs, lr, count, s);
+            if (c->trsv_mw)
+                launch_trsv32_mw(true, F, nb, D, ds, r1, r2, vs, lr, count, APM_STATUS_CHOL_B, s);
+            else
+                launch_trsv32_fused(true, F, nb, D, ds, r1, r2, vs, lr, count, s);
             check_launch();
             feed_chol_k(c);
-            launch_trsv32_fused(false, F, nb, D, ds, r2, r3, vs, lr, count, s);
+            if (c->trsv_mw)
+                launch_trsv32_mw(false, F, nb, D, ds, r2, r3, vs, lr, count, APM_STATUS_CHOL_B, s);
+            else
+                launch_trsv32_fused(false, F, nb, D, ds, r2, r3, vs, lr, count, s);
             check_launch();
         } else {
             for (int J = 0; J < nb; ++J) {
@@ -751,6 +762,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
+    if (const char* e = getenv("APM_OUTER32")) OUTER32 = std::max(1, atoi(e));
     if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
     if (const char* e = getenv("APM_SCHED")) {  // host wait policy of synchronisations
         const std::string m(e);
@@ -769,6 +781,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
+    if (const char* e = getenv("APM_TRSV_MW")) c->trsv_mw = atoi(e) != 0;
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs

@@ -967,6 +967,179 @@ __global__ __launch_bounds__(1024) void k_trsv32_fused(MatF A, int nb, const flo
     }
 }
 
+// ------------------------------------------------------- multi-workgroup TRSV (G workgroups/chain)
+// The solve of one chain split over G workgroups of 256 threads: workgroup g owns the block steps
+// s = g, g+G, g+2G, ... (FWD: J = s, BWD: J = nb-1-s) and, for its step, streams the block row's
+// tiles against the solution blocks of the earlier steps, taken from an LDS copy of the solution
+// that it refreshes from global memory. Steps hand over through the solution itself: `out` is
+// NaN-filled before the launch (k_nan_fill) and every element is published with an agent-scope
+// atomic store; readers poll each element they need with agent-scope atomic loads until it is not
+// NaN (no flags, no fences: each value carries its own readiness, and gfx950 agent-scope atomics
+// bypass the XCD-private L2). The contributions of all but the previous step's block are summed
+// before waiting for it, so the critical path per step is one hand-over, one tile and the 64x64
+// inverse product. Polling is bounded: a chain whose solution never appears (a NaN produced by the
+// factor) is marked failed instead of spinning. Waiting only on blocks of the same launch is safe:
+// the G workgroups of a chain need no other kernel to finish to become resident.
+#define TRM_G 4         // workgroups per chain
+#define TRM_SPIN (1 << 20)  // polls per element before the chain is declared failed
+__global__ __launch_bounds__(256) void k_nan_fill(double* out, int64_t vstride, int np,
+                                                  Live live) {
+    const int b = blockIdx.y;
+    if (!live32(live, b)) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < np) out[b * vstride + i] = __builtin_nan("");
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* Dinv,
+                                                   int64_t dstride, const double* r, double* out,
+                                                   int64_t vstride, Live live, int fail_code) {
+    const int b = blockIdx.x / TRM_G, g = blockIdx.x % TRM_G;
+    if (!live32(live, b)) return;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row = t >> 2, q = t & 3;  // tile row, 16-column quarter
+    extern __shared__ double trm_sm[];
+    double* xs = trm_sm;               // np: solution blocks fetched so far (solve order)
+    double* red = xs + nb * 64;        // 4 x 64 column-sum partials (BWD)
+    double* rj = red + 4 * 64;         // 64: right-hand side of the step
+    __shared__ int bad;
+    if (t == 0) bad = 0;
+    __syncthreads();  // `bad` is read by every poll loop
+    const float* Lb = A.base + b * A.cstride;
+    const float* Db = Dinv + b * dstride;
+    const double* rb = r + b * vstride;
+    double* ob = out + b * vstride;
+    auto blk = [&](int idx) { return FWD ? idx : nb - 1 - idx; };  // solve order -> block
+    // fetch solution blocks of solve-order indices [a, e) into LDS (polling)
+    auto fetch = [&](int a, int e) {
+        for (int x = t; x < (e - a) * 64; x += 256) {
+            const int I = blk(a + x / 64), o = I * 64 + (x & 63);
+            double v = __hip_atomic_load(ob + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int n = 0;
+            while (__builtin_isnan(v) && n < TRM_SPIN && !bad) {
+                __builtin_amdgcn_s_sleep(1);
+                v = __hip_atomic_load(ob + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ++n;
+            }
+            if (__builtin_isnan(v)) bad = 1;
+            xs[o] = v;
+        }
+    };
+    // 16-byte pieces of tile (J, I) (FWD: L_JI) or (I, J) (BWD: L_IJ) for this thread
+    auto piece = [&](int J, int I, int u) -> f4_t {
+        const int64_t o = FWD ? (int64_t)(J * 64 + row) * A.ld + I * 64 + 16 * q + 4 * u
+                              : (int64_t)(I * 64 + row) * A.ld + J * 64 + 16 * q + 4 * u;
+        return *reinterpret_cast<const f4_t*>(Lb + o);
+    };
+    int have = 0;  // solve-order blocks [0, have) are in LDS
+    for (int s = g; s < nb; s += TRM_G) {
+        const int J = blk(s);
+        double acc[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] = 0.0;
+        auto consume = [&](int I) {
+            f4_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = piece(J, I, u);
+            if (FWD) {
+                const double* x = xs + I * 64 + 16 * q;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[0] = fma((double)v[u][e], x[4 * u + e], acc[0]);
+            } else {
+                const double x = xs[I * 64 + row];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[4 * u + e] = fma((double)v[u][e], x, acc[4 * u + e]);
+            }
+        };
+        // all earlier blocks but the previous step's, then that one
+        const int early = s > 0 ? s - 1 : 0;
+        if (have < early) {
+            fetch(have, early);
+            have = early;
+        }
+        __syncthreads();
+        for (int idx = 0; idx < early; ++idx) consume(blk(idx));
+        if (s > 0) {
+            if (have < s) {
+                fetch(s - 1, s);
+                have = s;
+            }
+            __syncthreads();
+            consume(blk(s - 1));
+        }
+        if (FWD) {
+            double sum = acc[0];
+            sum += __shfl_xor(sum, 1, 64);
+            sum += __shfl_xor(sum, 2, 64);
+            if (q == 0) rj[row] = rb[J * 64 + row] - sum;
+        } else {  // column sums: lanes 4*(row%16) + q share columns 16q..16q+15
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                acc[c] += __shfl_xor(acc[c], 4, 64);
+                acc[c] += __shfl_xor(acc[c], 8, 64);
+                acc[c] += __shfl_xor(acc[c], 16, 64);
+                acc[c] += __shfl_xor(acc[c], 32, 64);
+            }
+            if (lane < 4) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) red[w * 64 + 16 * lane + c] = acc[c];
+            }
+            __syncthreads();
+            if (t < 64) rj[t] = rb[J * 64 + t] - (red[t] + red[64 + t] + red[128 + t] + red[192 + t]);
+        }
+        __syncthreads();
+        // x_J[c] = sum_m inv(L_JJ)[c][m] rj[m] (FWD) or inv(L_JJ)[m][c] rj[m] (BWD): thread (c, q)
+        // sums m = 16q .. 16q+15
+        {
+            const float* D = Db + (int64_t)J * 4096;
+            double sum = 0.0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = 16 * q + e;
+                sum = fma((double)(FWD ? D[row * 64 + m] : D[m * 64 + row]), rj[m], sum);
+            }
+            sum += __shfl_xor(sum, 1, 64);
+            sum += __shfl_xor(sum, 2, 64);
+            if (q == 0) {
+                xs[J * 64 + row] = sum;
+                __hip_atomic_store(ob + J * 64 + row, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0 && bad) live.status[b] = fail_code;
+}
+
+bool trsv32_mw_ok(int np) { return np <= TRF_MAXNP; }
+
+void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+                      const double* r, double* out, int64_t vstride, Live live, int nchains,
+                      int fail_code, hipStream_t s) {
+    const size_t lds = sizeof(double) * (nb * 64 + 4 * 64 + 64);
+    static bool attr = false;
+    if (!attr) {  // dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP)
+        const int mx = (int)(sizeof(double) * (TRF_MAXNP + 4 * 64 + 64));
+        (void)hipFuncSetAttribute((const void*)k_trsv32_mw<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        (void)hipFuncSetAttribute((const void*)k_trsv32_mw<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        attr = true;
+    }
+    const int np = nb * 64;
+    hipLaunchKernelGGL(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,
+                       np, live);
+    if (fwd)
+        hipLaunchKernelGGL(k_trsv32_mw<true>, dim3(nchains * TRM_G), dim3(256), lds, s, A, nb,
+                           Dinv, dstride, r, out, vstride, live, fail_code);
+    else
+        hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * TRM_G), dim3(256), lds, s, A, nb,
+                           Dinv, dstride, r, out, vstride, live, fail_code);
+}
+
 static size_t trf_lds_bytes(int nb) {
     return sizeof(double) * (2 * nb * 64 + 16 * 64 + 64) + sizeof(float) * 64 * TRF_DP;
 }
