@@ -30,6 +30,10 @@ METRIC = BASE_METRIC = 'MCMC iters/sec + ESS/sec on θ, GP-classif N=4096 N_imp=
 PEAK_F64_MFMA_TFLOPS = 78.6   # MI355X FP64 matrix, spec (not in MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_*_f32)
 PEAK_HBM_TBS = 8.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_F16_MFMA_TFLOPS = 2516.6  # MI355X_MICROARCH.md: BF16/FP16 matrix ~2.5 PF dense (spec)
+# fp16x3 emulation of the fp32 Newton updates: 3 fp16 MFMA flops per
+# fp32-equivalent flop, so its fp32-equivalent ceiling is a third of the fp16 peak
+PEAK_F16X3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 
 
 def parse():
@@ -107,18 +111,29 @@ def device_sync():
         pass
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per dispatch of `kernel` inside the timed region, from the newest committed
-    PMC pass of this bench (profiles/r*_pmc_traffic.json, written by tools/prof_window.py from
-    separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of the same command, with the
-    guide's gfx950 corrections). PMC counters cannot be read live inside this process."""
+def pmc_traffic(*kernels):
+    """HBM bytes per dispatch of the kernels (dispatch-weighted over the names given: the bench's
+    HIP-event timing of a roofline covers all launch variants of one operation) inside the timed
+    region, from the newest committed PMC pass of this bench (profiles/r*_pmc_traffic.json,
+    written by tools/prof_window.py from separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc
+    WRITE_SIZE` runs of the same command, with the guide's gfx950 corrections). PMC counters
+    cannot be read live inside this process."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
     if not files:
         return None, None
-    d = json.load(open(files[-1])).get('pmc_traffic', {}).get(kernel, {})
-    b = d.get('traffic_bytes_per_dispatch')
-    return b, (os.path.relpath(files[-1], REPO) if b is not None else None)
+    d = json.load(open(files[-1])).get('pmc_traffic', {})
+    tot = n = 0
+    for k in kernels:
+        e = d.get(k, {})
+        b = e.get('traffic_bytes_per_dispatch')
+        if b is not None:
+            cnt = e['FETCH_SIZE']['dispatches']
+            tot += b * cnt
+            n += cnt
+    if not n:
+        return None, None
+    return tot / n, os.path.relpath(files[-1], REPO)
 
 
 def timed_region(dist, step_fn, steps, on_start=None):
@@ -243,13 +258,13 @@ def main():
     ctx.prof_read(0, reset=True)
     _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
 
-    def mfma_roofline(name, kernel, peak, short):
+    def mfma_roofline(name, kernel, peak, shorts):
         ms, cnt, flops = prof[name]
         if not cnt:
             return None
         avg_s = ms * 1e-3 / cnt
         achieved = (flops / cnt) / avg_s / 1e12
-        tr, src = pmc_traffic(short)
+        tr, src = pmc_traffic(*shorts)
         return {'kernel': kernel, 'bound': 'mfma', 'achieved': achieved, 'peak': peak,
                 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': tr,
                 'traffic_unit': 'HBM bytes per launch', 'traffic_source': src,
@@ -257,12 +272,17 @@ def main():
                 'algorithmic_flops_per_launch': flops / cnt,
                 'share_of_step_time': (ms * 1e-3) / elapsed}
 
-    upd64 = mfma_roofline('chol_update', 'k_chol_update (f64 MFMA trailing update of the '
-                          'fp64 factorisations: chol(K), SYRK + chol of I + L_K^T W L_K)',
-                          PEAK_F64_MFMA_TFLOPS, 'k_chol_update')
-    upd32 = mfma_roofline('chol_update32', 'k_chol_update32 (f32 MFMA trailing update of the '
-                          'mixed-precision Newton factorisation of B)', PEAK_F32_MFMA_TFLOPS,
-                          'k_chol_update32')
+    upd64 = mfma_roofline('chol_update', 'k_chol_update_t128 + k_chol_update (f64 MFMA trailing '
+                          'updates of the fp64 factorisations: chol(K), SYRK + chol of '
+                          'I + L_K^T W L_K)', PEAK_F64_MFMA_TFLOPS,
+                          ('k_chol_update_t128', 'k_chol_update'))
+    upd32 = mfma_roofline('chol_update32', 'k_chol_update32_t128 + k_chol_update32 (trailing '
+                          'updates of the Newton factorisation of B, fp16x3: fp32 operands split '
+                          'into fp16 hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 '
+                          'accumulation; achieved in fp32-equivalent flops against the fp16 peak '
+                          '/ 3)', PEAK_F16X3_TFLOPS,
+                          ('k_chol_update32_t128<true>', 'k_chol_update32_t128<false>',
+                           'k_chol_update32'))
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])

@@ -230,6 +230,43 @@ def test_mixed_newton_matches_fp64(nat, monkeypatch):
         assert abs(o32[b] - o64[b]) <= 1e-6 * max(1.0, abs(o64[b])), (b, o32[b], o64[b])
 
 
+def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
+    """fp16x3 trailing updates of the Newton factor (chol32.hip, default) against fp32 operands
+    (APM_H3=0): same iteration counts, modes to 1e-9 relative, estimates to 1e-6; with a chain
+    at theta_0 >= 19 in the call the range guard keeps the whole call on fp32 operands
+    (bit-identical to APM_H3=0)."""
+    X, y, thetas, ns = _mixed_case()
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_H3=0)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    assert (s0 == 0).all() and (s1 == 0).all()
+    np.testing.assert_array_equal(n1, n0)
+    for b in range(len(thetas)):
+        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-9, atol=1e-9 * np.abs(f0[b]).max())
+        assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
+    big = thetas.copy()
+    big[2, 0] = 19.5
+    o0, s0, n0, f0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_H3=0)
+    o1, s1, n1, f1 = _run_is(nat, X, y, big, ns, monkeypatch)
+    np.testing.assert_array_equal(s1, s0)
+    np.testing.assert_array_equal(n1, n0)
+    for b in range(len(big)):
+        if s0[b] == 0:
+            np.testing.assert_array_equal(f1[b], f0[b])
+
+
+def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
+    """The Newton solves' 4-workgroup TRSV (k_trsv32_mw, default) against the one-workgroup
+    kernel (APM_TRSV_MW=0): modes to 1e-12 relative (summation order only)."""
+    X, y, thetas, ns = _mixed_case()
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_TRSV_MW=0)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    assert (s0 == 0).all() and (s1 == 0).all()
+    np.testing.assert_array_equal(n1, n0)
+    for b in range(len(thetas)):
+        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-12, atol=1e-12 * np.abs(f0[b]).max())
+        assert abs(o1[b] - o0[b]) <= 1e-9 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
+
+
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
 def test_mixed_newton_fp64_fallback(nat, monkeypatch, tol):
     """Chains whose refined fp32 solve fails the acceptance test are rerun in fp64 from f = 0
