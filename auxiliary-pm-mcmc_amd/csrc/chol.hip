@@ -369,6 +369,9 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
 // with the 16-byte pieces XOR-swizzled by row (piece p of row r at slot p ^ (r & 7)), so the
 // 16-byte fragment reads of 8 consecutive rows hit distinct banks.
 #define KS64T 16
+#ifndef T64_ABL
+#define T64_ABL 0
+#endif
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 struct __attribute__((aligned(16))) GemmSmem64T {
@@ -400,6 +403,9 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
     const double* gb = Ab + (int64_t)((wv < 2 ? cb0 : cb1) * 64 + (srow & 63)) * A.ld + k0 * 64 +
                        2 * spiece;
     auto glds = [&](int sidx, int buf) {
+#if T64_ABL == 2  // ablation (tools/upd64_bench.cpp): no operand loads
+        return;
+#endif
         const int o = sidx * KS64T;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -429,8 +435,12 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
                 for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
                     for (int bj = 0; bj < 4; ++bj)
+#if T64_ABL == 1  // ablation: no MFMA (loads + LDS + barriers only)
+                        acc[bi][bj][0] += a2[bi][q] * b2[bj][q];
+#else
                         acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
                             a2[bi][q], b2[bj][q], acc[bi][bj], 0, 0, 0);
+#endif
         }
     };
     const int nsub = (64 * kc) / KS64T;
