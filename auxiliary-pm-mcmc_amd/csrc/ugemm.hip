@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     const int sb = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
     const int r16 = lane & 15, kq = lane >> 4;
-    __shared__ float Ut[64][UP];
+    __shared__ float Ut[2][64][UP];
     __shared__ double csum[2][64];
 
     const int64_t slot = slots[b];
@@ -133,39 +133,48 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
 
-    for (int kk = 0; kk < kend; kk += 64) {
-        __syncthreads();
-        // stage U[kk:kk+64][sb*64 : sb*64+64] (16 KB) with 16-byte loads
+    // U[kk:kk+64][sb*64 : sb*64+64] (16 KB, 16-byte loads) and the A fragments (straight from
+    // global: 16 contiguous floats per lane and row) of the next slice are loaded into registers
+    // while the current one is multiplied; U goes through two LDS buffers, one barrier per slice
+    f4_t un[4];
+    f4_t an[2][4];
+    auto gload = [&](int kk) {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const int e = tid + h * 256;  // float4 index 0..1023
-            const int r = e >> 4, c4 = (e & 15) * 4;
-            const f4_t v = *reinterpret_cast<const f4_t*>(U + (int64_t)(kk + r) * sp + sb * 64 + c4);
-            Ut[r][c4] = v[0];
-            Ut[r][c4 + 1] = v[1];
-            Ut[r][c4 + 2] = v[2];
-            Ut[r][c4 + 3] = v[3];
+            un[h] = *reinterpret_cast<const f4_t*>(U + (int64_t)(kk + (e >> 4)) * sp + sb * 64 +
+                                                   (e & 15) * 4);
         }
-        // A fragments straight from global: 16 contiguous floats per lane and row
-        float a[2][16];
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
             const float* p = L + (int64_t)(i * 64 + 32 * wr + 16 * bi + r16) * np + kk + kq * 16;
 #pragma unroll
-            for (int t = 0; t < 16; t += 4) {
-                const f4_t v = *reinterpret_cast<const f4_t*>(p + t);
-                a[bi][t] = v[0];
-                a[bi][t + 1] = v[1];
-                a[bi][t + 2] = v[2];
-                a[bi][t + 3] = v[3];
-            }
+            for (int t = 0; t < 4; ++t) an[bi][t] = *reinterpret_cast<const f4_t*>(p + 4 * t);
         }
+    };
+    gload(0);
+    for (int kk = 0, cur = 0; kk < kend; kk += 64, cur ^= 1) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int e = tid + h * 256;
+            const int r = e >> 4, c4 = (e & 15) * 4;
+            Ut[cur][r][c4] = un[h][0];
+            Ut[cur][r][c4 + 1] = un[h][1];
+            Ut[cur][r][c4 + 2] = un[h][2];
+            Ut[cur][r][c4 + 3] = un[h][3];
+        }
+        float a[2][16];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) a[bi][t] = an[bi][t >> 2][t & 3];
         __syncthreads();
+        if (kk + 64 < kend) gload(kk + 64);
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             float bv[2];
 #pragma unroll
-            for (int bj = 0; bj < 2; ++bj) bv[bj] = Ut[kq * 16 + t][32 * wc + 16 * bj + r16];
+            for (int bj = 0; bj < 2; ++bj) bv[bj] = Ut[cur][kq * 16 + t][32 * wc + 16 * bj + r16];
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
