@@ -56,7 +56,10 @@ struct apm_ctx {
     int* refining = nullptr;  // chains still refining their Newton solve
     double* refine_prev = nullptr;  // max|d| of the previous refinement step per chain
     int64_t n_refine_steps = 0, n_fp64_rerun = 0;  // statistics (apm_prof_read APM_PROF_STATS)
-    int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;
+    int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;  // d_ubufs = d_slots + B
+    // pinned host staging of the per-call transfers (one H2D of slots + ubufs, D2H copies that
+    // are enqueued together and waited on once): [B slots][B ubufs][B out][B status][B n_iter]
+    char* hpin = nullptr;
     double *d_ca = nullptr, *d_cb = nullptr;
     uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
     double* U64 = nullptr;
@@ -386,6 +389,23 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
 
 void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
 
+// slots / ubufs of a call -> device in one copy from pinned memory
+void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubufs) {
+    int64_t* h = reinterpret_cast<int64_t*>(c->hpin);
+    const int B = c->max_batch;
+    if (slots) std::memcpy(h, slots, sizeof(int64_t) * count);
+    if (ubufs) std::memcpy(h + B, ubufs, sizeof(int64_t) * count);
+    if (ubufs)
+        HIPC(hipMemcpyAsync(c->d_slots, h, sizeof(int64_t) * (B + count), hipMemcpyHostToDevice,
+                            c->stream));
+    else if (slots)
+        HIPC(hipMemcpyAsync(c->d_slots, h, sizeof(int64_t) * count, hipMemcpyHostToDevice,
+                            c->stream));
+}
+double* pin_out(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 16 * c->max_batch); }
+int* pin_status(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 32 * c->max_batch); }
+int* pin_iter(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 36 * c->max_batch); }
+
 void u_eval_device(apm_ctx* c, int count) {
     {
         ProfScope ps(c, APM_PROF_UGEMM, (double)c->n * (c->n + 1) * c->S * count);
@@ -476,9 +496,10 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         ++c->n_refine_steps;
         if (last) break;
-        HIPC(hipMemcpyAsync(ref_h.data(), c->refining, sizeof(int) * count,
+        HIPC(hipMemcpyAsync(pin_iter(c), c->refining, sizeof(int) * count,
                             hipMemcpyDeviceToHost, s));
         sync(c);
+        std::memcpy(ref_h.data(), pin_iter(c), sizeof(int) * count);
         bool any = false;
         for (int b = 0; b < count; ++b) any |= ref_h[b] != 0;
         if (!any) break;
@@ -529,11 +550,13 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
         launch_newton_check(c->v, c->n, c->np, c->tol, c->active, c->status, c->n_iter, count,
                             c->stream);
         check_launch();
-        HIPC(hipMemcpyAsync(act.data(), c->active, sizeof(int) * count, hipMemcpyDeviceToHost,
+        HIPC(hipMemcpyAsync(pin_iter(c), c->active, sizeof(int) * count, hipMemcpyDeviceToHost,
                             c->stream));
-        HIPC(hipMemcpyAsync(st_h.data(), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
-                            c->stream));
+        HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count,
+                            hipMemcpyDeviceToHost, c->stream));
         sync(c);
+        std::memcpy(act.data(), pin_iter(c), sizeof(int) * count);
+        std::memcpy(st_h.data(), pin_status(c), sizeof(int) * count);
         bool any = false;
         for (int b = 0; b < count; ++b) any |= (act[b] != 0 && st_h[b] == 0);
         if (!any) break;
@@ -731,13 +754,16 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             u_eval_device(c, count);
         }
     }
-    HIPC(hipMemcpyAsync(out_logf, c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
+    HIPC(hipMemcpyAsync(pin_out(c), c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
                         c->stream));
-    HIPC(hipMemcpyAsync(st_h.data(), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
+    HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
                         c->stream));
-    HIPC(hipMemcpyAsync(it_h.data(), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
+    HIPC(hipMemcpyAsync(pin_iter(c), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
                         c->stream));
     sync(c);
+    std::memcpy(out_logf, pin_out(c), sizeof(double) * count);
+    std::memcpy(st_h.data(), pin_status(c), sizeof(int) * count);
+    std::memcpy(it_h.data(), pin_iter(c), sizeof(int) * count);
     for (int b = 0; b < count; ++b) {
         status[b] = st_h[b];
         if (nops) {
@@ -845,8 +871,9 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->active2 = dalloc<int>(c, B);
     c->status2 = dalloc<int>(c, B);
     c->refine_prev = dalloc<double>(c, B);
-    c->d_slots = dalloc<int64_t>(c, B);
-    c->d_ubufs = dalloc<int64_t>(c, B);
+    c->d_slots = dalloc<int64_t>(c, 2 * B);
+    c->d_ubufs = c->d_slots + B;
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 40, hipHostMallocDefault));
     c->d_i3 = dalloc<int64_t>(c, 3 * B);
     c->d_ca = dalloc<double>(c, B);
     c->d_cb = dalloc<double>(c, B);
@@ -867,6 +894,7 @@ void free_ctx(apm_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
+    if (c->hpin) (void)hipHostFree(c->hpin);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1039,12 +1067,7 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
         // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip)
         c->h3_now = c->h3;
         for (int64_t b = 0; b < count; ++b) c->h3_now &= th[b * c->P] < 19.0;
-        if (est != APM_EST_LAPLACE) {
-            HIPC(hipMemcpyAsync(c->d_slots, slots, sizeof(int64_t) * count, hipMemcpyHostToDevice,
-                                c->stream));
-            HIPC(hipMemcpyAsync(c->d_ubufs, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
-                                c->stream));
-        }
+        if (est != APM_EST_LAPLACE) upload_idx(c, (int)count, slots, ubufs);
         theta_eval_impl(c, est, (int)count, true, out_logf, status, nops);
     } catch (const HipError& e) {
         return fail(c, APM_E_HIP, e.msg);
@@ -1090,17 +1113,16 @@ int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* u
         return APM_E_INVALID;
     try {
         HIPC(hipSetDevice(c->device));
-        HIPC(hipMemcpyAsync(c->d_slots, slots, sizeof(int64_t) * count, hipMemcpyHostToDevice,
-                            c->stream));
-        HIPC(hipMemcpyAsync(c->d_ubufs, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
-                            c->stream));
+        upload_idx(c, (int)count, slots, ubufs);
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
         u_eval_device(c, (int)count);
-        HIPC(hipMemcpyAsync(out_logf, c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
+        HIPC(hipMemcpyAsync(pin_out(c), c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
                             c->stream));
-        HIPC(hipMemcpyAsync(status, c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
-                            c->stream));
+        HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count,
+                            hipMemcpyDeviceToHost, c->stream));
         sync(c);
+        std::memcpy(out_logf, pin_out(c), sizeof(double) * count);
+        std::memcpy(status, pin_status(c), sizeof(int) * count);
     } catch (const HipError& e) {
         return fail(c, APM_E_HIP, e.msg);
     }
