@@ -163,9 +163,18 @@ __global__ __launch_bounds__(256) void k_copy_lower(MatB src, MatB dst, Live liv
     tri_decode(blockIdx.x, ti, tj);
     const double* S = src.base + b * src.cstride;
     double* D = dst.base + b * dst.cstride;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
-        D[(int64_t)r * dst.ld + c] = S[(int64_t)r * src.ld + c];
+    d2_t v[8];  // 16-byte pieces, all loads in flight before the stores
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h;  // piece: row e / 32, columns 2 (e % 32) .. +1
+        const int r = ti * 64 + (e >> 5), c = tj * 64 + 2 * (e & 31);
+        v[h] = *reinterpret_cast<const d2_t*>(S + (int64_t)r * src.ld + c);
+    }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h;
+        const int r = ti * 64 + (e >> 5), c = tj * 64 + 2 * (e & 31);
+        *reinterpret_cast<d2_t*>(D + (int64_t)r * dst.ld + c) = v[h];
     }
 }
 

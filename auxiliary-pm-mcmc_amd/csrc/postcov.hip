@@ -61,23 +61,39 @@ __global__ __launch_bounds__(256) void k_form_y2(MatB src, MatB dst, int64_t dco
     const int ta = blockIdx.x / nb, tk = blockIdx.x % nb;
     const int np = nb * 64;
     double* D = dst.base + b * dst.cstride + (int64_t)(ta * 64) * dst.ld + dcol0 + tk * 64;
+    // 16-byte pieces: thread t, step h handles row (t + 256h) / 32, columns 2 ((t + 256h) % 32) .. +1
     if (tk > ta) {  // upper tiles are read as zeros by the SYRK's panel-wide k-range
-        for (int e = threadIdx.x; e < 4096; e += 256) D[(int64_t)(e >> 6) * dst.ld + (e & 63)] = 0.0;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const int e = threadIdx.x + 256 * h;
+            *reinterpret_cast<d2_t*>(D + (int64_t)(e >> 5) * dst.ld + 2 * (e & 31)) = d2_t{0.0, 0.0};
+        }
         return;
     }
     const int sr = nb - 1 - tk, sc = nb - 1 - ta;  // source tile (lower: sr >= sc)
     __shared__ double T[64][65];
     const double* S = src.base + b * src.cstride + (int64_t)(sr * 64) * src.ld + sc * 64;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        T[r][c] = (sr > sc || c <= r) ? S[(int64_t)r * src.ld + c] : 0.0;
+    d2_t v[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h;
+        v[h] = *reinterpret_cast<const d2_t*>(S + (int64_t)(e >> 5) * src.ld + 2 * (e & 31));
+    }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
+        T[r][c] = (sr > sc || c <= r) ? v[h].x : 0.0;
+        T[r][c + 1] = (sr > sc || c + 1 <= r) ? v[h].y : 0.0;
     }
     __syncthreads();
     const double* w = Ws + b * vstride;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int al = e >> 6, kl = e & 63;  // local output row (a) and column (k')
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h;
+        const int al = e >> 5, kl = 2 * (e & 31);  // local output row (a) and columns (k', k'+1)
         const int kg = tk * 64 + kl;
-        D[(int64_t)al * dst.ld + kl] = w[np - 1 - kg] * T[63 - kl][63 - al];
+        *reinterpret_cast<d2_t*>(D + (int64_t)al * dst.ld + kl) =
+            d2_t{w[np - 1 - kg] * T[63 - kl][63 - al], w[np - 2 - kg] * T[62 - kl][63 - al]};
     }
 }
 
@@ -92,18 +108,22 @@ void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t
 __global__ __launch_bounds__(256) void k_reverse_cols(MatB M, int np, Live live) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
+    // thread: columns (c, c+1) and their mirrors (c2-1, c2), c even, 16-byte accesses
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int half = np / 2;
-    if (e >= (int64_t)np * half) return;
-    const int i = (int)(e / half), c = (int)(e % half), c2 = np - 1 - c;
+    const int quarter = np / 4;
+    if (e >= (int64_t)np * quarter) return;
+    const int i = (int)(e / quarter), c = 2 * (int)(e % quarter), c2 = np - 1 - c;
     double* row = M.base + b * M.cstride + (int64_t)i * M.ld;
-    const double l1 = (c <= i) ? row[c] : 0.0, l2 = (c2 <= i) ? row[c2] : 0.0;
-    row[c] = l2;
-    row[c2] = l1;
+    const d2_t lo = *reinterpret_cast<const d2_t*>(row + c);        // columns c, c+1
+    const d2_t hi = *reinterpret_cast<const d2_t*>(row + c2 - 1);   // columns c2-1, c2
+    const double a0 = (c <= i) ? lo.x : 0.0, a1 = (c + 1 <= i) ? lo.y : 0.0;
+    const double b0 = (c2 - 1 <= i) ? hi.x : 0.0, b1 = (c2 <= i) ? hi.y : 0.0;
+    *reinterpret_cast<d2_t*>(row + c) = d2_t{b1, b0};
+    *reinterpret_cast<d2_t*>(row + c2 - 1) = d2_t{a1, a0};
 }
 
 void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s) {
-    const int64_t tot = (int64_t)np * (np / 2);
+    const int64_t tot = (int64_t)np * (np / 4);
     hipLaunchKernelGGL(k_reverse_cols, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0,
                        s, M, np, live);
 }
@@ -117,9 +137,11 @@ __global__ __launch_bounds__(256) void k_identity_lower(MatB M, Live live) {
     while ((ti + 1) * (ti + 2) / 2 <= (int)blockIdx.x) ++ti;
     const int tj = blockIdx.x - ti * (ti + 1) / 2;
     double* D = M.base + b * M.cstride + (int64_t)(ti * 64) * M.ld + tj * 64;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        D[(int64_t)r * M.ld + c] = (ti == tj && r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
+        *reinterpret_cast<d2_t*>(D + (int64_t)r * M.ld + c) =
+            d2_t{(ti == tj && r == c) ? 1.0 : 0.0, (ti == tj && r == c + 1) ? 1.0 : 0.0};
     }
 }
 
@@ -141,9 +163,20 @@ __global__ __launch_bounds__(256) void k_trmv_lt(MatB L, const double* __restric
     const int c = cb * 64 + lane;
     const double* Lb = L.base + b * L.cstride;
     const double* hb = h + b * vstride;
-    double s = 0.0;
-    for (int r = cb * 64 + w; r < np; r += 4)
-        if (r >= c) s += Lb[(int64_t)r * L.ld + c] * hb[REV ? np - 1 - r : r];
+    // 8 rows in flight per wave (independent partial sums), rows r >= c only
+    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int r = cb * 64 + w;
+    for (; r + 28 < np; r += 32) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int rr = r + 4 * u;
+            const double lv = Lb[(int64_t)rr * L.ld + c];
+            s8[u] += (rr >= c) ? lv * hb[REV ? np - 1 - rr : rr] : 0.0;
+        }
+    }
+    for (; r < np; r += 4)
+        if (r >= c) s8[0] += Lb[(int64_t)r * L.ld + c] * hb[REV ? np - 1 - r : r];
+    const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     __shared__ double red[4][64];
     red[w][lane] = s;
     __syncthreads();
