@@ -108,22 +108,18 @@ void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t
 __global__ __launch_bounds__(256) void k_reverse_cols(MatB M, int np, Live live) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
-    // thread: columns (c, c+1) and their mirrors (c2-1, c2), c even, 16-byte accesses
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int quarter = np / 4;
-    if (e >= (int64_t)np * quarter) return;
-    const int i = (int)(e / quarter), c = 2 * (int)(e % quarter), c2 = np - 1 - c;
+    const int half = np / 2;
+    if (e >= (int64_t)np * half) return;
+    const int i = (int)(e / half), c = (int)(e % half), c2 = np - 1 - c;
     double* row = M.base + b * M.cstride + (int64_t)i * M.ld;
-    const d2_t lo = *reinterpret_cast<const d2_t*>(row + c);        // columns c, c+1
-    const d2_t hi = *reinterpret_cast<const d2_t*>(row + c2 - 1);   // columns c2-1, c2
-    const double a0 = (c <= i) ? lo.x : 0.0, a1 = (c + 1 <= i) ? lo.y : 0.0;
-    const double b0 = (c2 - 1 <= i) ? hi.x : 0.0, b1 = (c2 <= i) ? hi.y : 0.0;
-    *reinterpret_cast<d2_t*>(row + c) = d2_t{b1, b0};
-    *reinterpret_cast<d2_t*>(row + c2 - 1) = d2_t{a1, a0};
+    const double l1 = (c <= i) ? row[c] : 0.0, l2 = (c2 <= i) ? row[c2] : 0.0;
+    row[c] = l2;
+    row[c2] = l1;
 }
 
 void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s) {
-    const int64_t tot = (int64_t)np * (np / 4);
+    const int64_t tot = (int64_t)np * (np / 2);
     hipLaunchKernelGGL(k_reverse_cols, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0,
                        s, M, np, live);
 }
