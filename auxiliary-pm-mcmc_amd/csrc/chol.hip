@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_
                                                   int fail_code) {
     const int b = blockIdx.x;
     if (!chain_live(live, b)) return;
-    __shared__ DiagSmem S;
+    __shared__ DiagSmemT<TS> S;  // fp32 tiles (Newton matrix): fp32 arithmetic
     const int lane = threadIdx.x;
     TS* At = A.base + b * A.cstride + (int64_t)(k * 64) * A.ld + k * 64;
     // 64x64 tile -> LDS: 4 rounds of 8 independent 2-element loads per lane (lane: 2 columns)

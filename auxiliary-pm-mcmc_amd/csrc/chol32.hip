@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
-        DiagSmem d;
+        DiagSmem32 d;  // fp32 arithmetic: the Newton factor is refined in fp64
     } sm;
     int b, t;
     const bool fused = fd.enabled && (int)blockIdx.x < nchains;
@@ -283,10 +283,10 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 sm.d.T[(32 * wr + 16 * bi + F32_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
-                       (lane & 15)] = (double)acc[bi][bj][r];
+                       (lane & 15)] = acc[bi][bj][r];
     __syncthreads();
     if (wv == 0) {
-        const bool ok = diag_compute<true>(sm.d, lane);
+        const bool ok = diag_compute<true, float>(sm.d, lane);
         if (lane == 0) sm.d.ok = ok;
     }
     __syncthreads();
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
     __shared__ union {
         GemmSmem128 g;
         GemmSmemH3 h;
-        DiagSmem d;
+        DiagSmem32 d;  // fp32 arithmetic: the Newton factor is refined in fp64
     } sm;
     int b, t;
     const bool fused = fd.enabled && (int)blockIdx.x < nchains;
@@ -554,11 +554,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     sm.d.T[(16 * bi + F32_CROW(lane, r)) * DP + 16 * bj + r16] =
-                        (double)acc[bi][bj][r];
+                        acc[bi][bj][r];
     }
     __syncthreads();
     if (wv == 0) {
-        const bool ok = diag_compute<true>(sm.d, lane);
+        const bool ok = diag_compute<true, float>(sm.d, lane);
         if (lane == 0) sm.d.ok = ok;
     }
     __syncthreads();
