@@ -60,6 +60,8 @@ struct apm_ctx {
     // pinned host staging of the per-call transfers (one H2D of slots + ubufs, D2H copies that
     // are enqueued together and waited on once): [B slots][B ubufs][B out][B status][B n_iter]
     char* hpin = nullptr;
+    int64_t* hblk = nullptr;  // pinned mirror of the d_i3 .. d_ctrs block (apm_u_normal/combine)
+    double* hth = nullptr;    // pinned theta staging (B x P)
     double *d_ca = nullptr, *d_cb = nullptr;
     uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
     double* U64 = nullptr;
@@ -874,11 +876,16 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 40, hipHostMallocDefault));
-    c->d_i3 = dalloc<int64_t>(c, 3 * B);
-    c->d_ca = dalloc<double>(c, B);
-    c->d_cb = dalloc<double>(c, B);
-    c->d_seeds = dalloc<uint64_t>(c, B);
-    c->d_ctrs = dalloc<uint64_t>(c, B);
+    // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:
+    // [i3: 3B int64][ca: B][cb: B][seeds: B][ctrs: B]
+    c->d_i3 = dalloc<int64_t>(c, 7 * B);
+    c->d_ca = reinterpret_cast<double*>(c->d_i3 + 3 * B);
+    c->d_cb = c->d_ca + B;
+    c->d_seeds = reinterpret_cast<uint64_t*>(c->d_i3 + 5 * B);
+    c->d_ctrs = c->d_seeds + B;
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hblk), (size_t)B * 56, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hth),
+                       sizeof(double) * (size_t)B * std::max(c->P, 1), hipHostMallocDefault));
     c->U64 = dalloc<double>(c, n * S);
     const int64_t Lsz = (np + 64) * np;
     c->Sl = SlotSet{dalloc<float>(c, n_slots * Lsz), dalloc<float>(c, n_slots * np),
@@ -895,6 +902,8 @@ void free_ctx(apm_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->hpin) (void)hipHostFree(c->hpin);
+    if (c->hblk) (void)hipHostFree(c->hblk);
+    if (c->hth) (void)hipHostFree(c->hth);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1003,11 +1012,11 @@ int apm_u_normal(apm_ctx* c, int64_t count, const int64_t* ubufs, const uint64_t
     if (!check_idx(c, count, ubufs, c->n_ubufs, "ubuf")) return APM_E_INVALID;
     try {
         HIPC(hipSetDevice(c->device));
-        HIPC(hipMemcpyAsync(c->d_i3, ubufs, sizeof(int64_t) * count, hipMemcpyHostToDevice,
-                            c->stream));
-        HIPC(hipMemcpyAsync(c->d_seeds, seeds, sizeof(uint64_t) * count, hipMemcpyHostToDevice,
-                            c->stream));
-        HIPC(hipMemcpyAsync(c->d_ctrs, counters, sizeof(uint64_t) * count, hipMemcpyHostToDevice,
+        const int64_t B = c->max_batch;
+        std::memcpy(c->hblk, ubufs, sizeof(int64_t) * count);
+        std::memcpy(c->hblk + 5 * B, seeds, sizeof(uint64_t) * count);
+        std::memcpy(c->hblk + 6 * B, counters, sizeof(uint64_t) * count);
+        HIPC(hipMemcpyAsync(c->d_i3, c->hblk, sizeof(int64_t) * 7 * B, hipMemcpyHostToDevice,
                             c->stream));
         launch_u_normal(c->Up, c->d_i3, c->d_seeds, c->d_ctrs, c->n, c->S, (int)count,
                         c->stream);
@@ -1028,13 +1037,14 @@ int apm_u_combine(apm_ctx* c, int64_t count, const int64_t* dst, const int64_t* 
         return APM_E_INVALID;
     try {
         HIPC(hipSetDevice(c->device));
-        HIPC(hipMemcpyAsync(c->d_i3, dst, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
-        HIPC(hipMemcpyAsync(c->d_i3 + c->max_batch, a, sizeof(int64_t) * count,
-                            hipMemcpyHostToDevice, c->stream));
-        HIPC(hipMemcpyAsync(c->d_i3 + 2 * c->max_batch, b, sizeof(int64_t) * count,
-                            hipMemcpyHostToDevice, c->stream));
-        HIPC(hipMemcpyAsync(c->d_ca, ca, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
-        HIPC(hipMemcpyAsync(c->d_cb, cb, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+        const int64_t B = c->max_batch;
+        std::memcpy(c->hblk, dst, sizeof(int64_t) * count);
+        std::memcpy(c->hblk + B, a, sizeof(int64_t) * count);
+        std::memcpy(c->hblk + 2 * B, b, sizeof(int64_t) * count);
+        std::memcpy(c->hblk + 3 * B, ca, sizeof(double) * count);
+        std::memcpy(c->hblk + 4 * B, cb, sizeof(double) * count);
+        HIPC(hipMemcpyAsync(c->d_i3, c->hblk, sizeof(int64_t) * 5 * B, hipMemcpyHostToDevice,
+                            c->stream));
         launch_u_combine(c->Up, c->d_i3, c->d_i3 + c->max_batch, c->d_i3 + 2 * c->max_batch,
                          c->d_ca, c->d_cb, c->n, c->S, (int)count, c->stream);
         check_launch();
@@ -1059,10 +1069,10 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
     }
     try {
         HIPC(hipSetDevice(c->device));
-        std::vector<double> th((size_t)count * c->P);
+        double* th = c->hth;  // pinned: the upload is asynchronous
         for (int64_t b = 0; b < count; ++b)
             for (int p = 0; p < c->P; ++p) th[b * c->P + p] = thetas[b * ldt + p];
-        HIPC(hipMemcpyAsync(c->theta, th.data(), sizeof(double) * th.size(), hipMemcpyHostToDevice,
+        HIPC(hipMemcpyAsync(c->theta, th, sizeof(double) * count * c->P, hipMemcpyHostToDevice,
                             c->stream));
         // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip)
         c->h3_now = c->h3;
