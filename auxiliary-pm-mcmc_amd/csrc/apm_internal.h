@@ -182,6 +182,9 @@ void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int
 // out = L^T x (L lower, no reversal)
 void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int np, Live live,
                     int nchains, hipStream_t s);
+// the same products (and the REV form) tile-parallel through nb*nb*64 partials per chain
+void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,
+                       double* part, int64_t pstride, Live live, int nchains, hipStream_t s);
 // status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)
 void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s);
 

@@ -666,7 +666,8 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     MatB TL = c->A;
     MatB BL = bl_of(c);
     if (have_lk) {
-        launch_trmv_lt(BL, c->v.a, c->v.z, vs, np, lv, count, s);          // h = L_K^T a -> z
+        launch_trmv_tiles(false, BL, c->v.a, c->v.z, vs, np, c->sympart, c->sstride, lv, count,
+                          s);                                                 // h = L_K^T a -> z
         check_launch();
     } else {
         launch_copy_lower(c->K, BL, np, lv, count, s);
@@ -688,7 +689,8 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
         tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, true, count);
     }
     chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
-    launch_trmv_lt_rev(TL, c->v.z, c->v.Kb, vs, np, lv, count, s);       // g = J L'^T J h
+    launch_trmv_tiles(true, TL, c->v.z, c->v.Kb, vs, np, c->sympart, c->sstride, lv, count,
+                      s);                                                     // g = J L'^T J h
     check_launch();
 }
 

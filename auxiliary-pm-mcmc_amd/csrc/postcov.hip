@@ -193,6 +193,98 @@ void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int n
                        vstride, np, live);
 }
 
+// The same products from K's lower tiles in parallel (the kernel above walks a whole column strip
+// per workgroup, 64-KB-strided rows): workgroup (ti, tj), ti >= tj, loads its tile into registers
+// (thread: rows 4rg..+3, columns 4cg..+3, 16-byte loads) and writes the column partials
+// sum_r L[r][c] x(r) of the tile (lower part only on the diagonal) to part[tj][ti]; k_trmv_reduce
+// adds them over ti in a fixed order (deterministic). x(r) = REV ? h[np-1-r] : x[r].
+template <bool REV>
+__global__ __launch_bounds__(256) void k_trmv_part(MatB L, const double* __restrict__ x,
+                                                   int64_t vstride, double* __restrict__ part,
+                                                   int64_t pstride, int nb, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int t = blockIdx.x;
+    int ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > t) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    const int tj = t - ti * (ti + 1) / 2;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rg = tid >> 4, cg = tid & 15;
+    const int np = nb * 64;
+    const double* Lt = L.base + b * L.cstride + (int64_t)(ti * 64 + 4 * rg) * L.ld + tj * 64 + 4 * cg;
+    d2_t v[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[r][0] = *reinterpret_cast<const d2_t*>(Lt + (int64_t)r * L.ld);
+        v[r][1] = *reinterpret_cast<const d2_t*>(Lt + (int64_t)r * L.ld + 2);
+    }
+    const double* xb = x + b * vstride;
+    double xv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int gr = ti * 64 + 4 * rg + r;
+        xv[r] = xb[REV ? np - 1 - gr : gr];
+    }
+    const bool diag = ti == tj;
+    double cs[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double lv = c < 2 ? (c == 0 ? v[r][0].x : v[r][0].y) : (c == 2 ? v[r][1].x : v[r][1].y);
+            if (!diag || 4 * rg + r >= 4 * cg + c) s = fma(lv, xv[r], s);
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        cs[c] = s;
+    }
+    __shared__ double red[4][64];
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[w][4 * lane + c] = cs[c];
+    }
+    __syncthreads();
+    if (tid < 64)
+        part[b * pstride + ((int64_t)tj * nb + ti) * 64 + tid] =
+            red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+template <bool REV>
+__global__ __launch_bounds__(256) void k_trmv_reduce(const double* __restrict__ part,
+                                                     int64_t pstride, int nb,
+                                                     double* __restrict__ out, int64_t vstride,
+                                                     Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int np = nb * 64;
+    if (c >= np) return;
+    const int tj = c >> 6;
+    const double* pb = part + b * pstride + (int64_t)tj * nb * 64 + (c & 63);
+    double s = 0.0;
+    for (int ti = tj; ti < nb; ++ti) s += pb[(int64_t)ti * 64];
+    out[b * vstride + (REV ? np - 1 - c : c)] = s;
+}
+
+void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,
+                       double* part, int64_t pstride, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    const dim3 gp(nb * (nb + 1) / 2, nchains), gr((np + 255) / 256, nchains);
+    if (rev) {
+        hipLaunchKernelGGL(k_trmv_part<true>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
+                           nb, live);
+        hipLaunchKernelGGL(k_trmv_reduce<true>, gr, dim3(256), 0, s, part, pstride, nb, out,
+                           vstride, live);
+    } else {
+        hipLaunchKernelGGL(k_trmv_part<false>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
+                           nb, live);
+        hipLaunchKernelGGL(k_trmv_reduce<false>, gr, dim3(256), 0, s, part, pstride, nb, out,
+                           vstride, live);
+    }
+}
+
 __global__ void k_merge_status(int* status, const int* other, int code, int nchains) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nchains && other[b] != 0) status[b] = code;
