@@ -177,12 +177,7 @@ void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t
                     Live live, int nchains, hipStream_t s);
 void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s);
 void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s);
-void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
-                        int nchains, hipStream_t s);
-// out = L^T x (L lower, no reversal)
-void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int np, Live live,
-                    int nchains, hipStream_t s);
-// the same products (and the REV form) tile-parallel through nb*nb*64 partials per chain
+// out = L^T x (L lower), or with rev g = J L^T J h; tile-parallel through nb*nb*64 partials per chain
 void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,
                        double* part, int64_t pstride, Live live, int nchains, hipStream_t s);
 // status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)

@@ -147,54 +147,8 @@ void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s
 }
 
 // g = J L'^T J h: g[np-1-c] = sum_{r >= c} L'[r][c] h[np-1-r] (REV), or out[c] = sum_{r >= c}
-// L[r][c] x[r] (h = L_K^T a); one workgroup per 64-column block, each wave strides over rows
-// (512-byte coalesced row segments), waves reduced through LDS.
-template <bool REV>
-__global__ __launch_bounds__(256) void k_trmv_lt(MatB L, const double* __restrict__ h,
-                                                 double* __restrict__ g, int64_t vstride, int np,
-                                                 Live live) {
-    const int b = blockIdx.y;
-    if (!live_pc(live, b)) return;
-    const int cb = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = cb * 64 + lane;
-    const double* Lb = L.base + b * L.cstride;
-    const double* hb = h + b * vstride;
-    // 8 rows in flight per wave (independent partial sums), rows r >= c only
-    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int r = cb * 64 + w;
-    for (; r + 28 < np; r += 32) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int rr = r + 4 * u;
-            const double lv = Lb[(int64_t)rr * L.ld + c];
-            s8[u] += (rr >= c) ? lv * hb[REV ? np - 1 - rr : rr] : 0.0;
-        }
-    }
-    for (; r < np; r += 4)
-        if (r >= c) s8[0] += Lb[(int64_t)r * L.ld + c] * hb[REV ? np - 1 - r : r];
-    const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-    __shared__ double red[4][64];
-    red[w][lane] = s;
-    __syncthreads();
-    if (w == 0)
-        g[b * vstride + (REV ? np - 1 - c : c)] =
-            red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-}
-
-void launch_trmv_lt_rev(MatB L, const double* h, double* g, int64_t vstride, int np, Live live,
-                        int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_trmv_lt<true>, dim3(np / 64, nchains), dim3(256), 0, s, L, h, g, vstride,
-                       np, live);
-}
-
-void launch_trmv_lt(MatB L, const double* x, double* out, int64_t vstride, int np, Live live,
-                    int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_trmv_lt<false>, dim3(np / 64, nchains), dim3(256), 0, s, L, x, out,
-                       vstride, np, live);
-}
-
-// The same products from K's lower tiles in parallel (the kernel above walks a whole column strip
-// per workgroup, 64-KB-strided rows): workgroup (ti, tj), ti >= tj, loads its tile into registers
+// L[r][c] x[r] (h = L_K^T a), from L's lower tiles in parallel (a workgroup per column strip
+// walks 64-KB-strided rows and leaves most CUs idle): workgroup (ti, tj), ti >= tj, loads its tile into registers
 // (thread: rows 4rg..+3, columns 4cg..+3, 16-byte loads) and writes the column partials
 // sum_r L[r][c] x(r) of the tile (lower part only on the diagonal) to part[tj][ti]; k_trmv_reduce
 // adds them over ti in a fixed order (deterministic). x(r) = REV ? h[np-1-r] : x[r].
