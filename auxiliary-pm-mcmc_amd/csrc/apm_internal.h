@@ -173,9 +173,9 @@ void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t 
                     Live live, int nchains, hipStream_t s);
 void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Live live,
                     int nchains, hipStream_t s);
-void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride, int np,
-                    Live live, int nchains, hipStream_t s);
-void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s);
+// dst (from column dcol0) <- Y2 = J (W^1/2 L)^T J, and L <- L J in place, in one pass
+void launch_form_y2_rev(MatB L, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride,
+                        int np, Live live, int nchains, hipStream_t s);
 void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s);
 // out = L^T x (L lower), or with rev g = J L^T J h; tile-parallel through nb*nb*64 partials per chain
 void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,

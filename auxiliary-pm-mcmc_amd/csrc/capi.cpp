@@ -678,9 +678,7 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
         launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
         check_launch();
     }
-    launch_form_y2(BL, TL, np, c->v.Ws, vs, np, lv, count, s);           // Y2 = J Z^T J
-    check_launch();
-    launch_reverse_cols(BL, np, lv, count, s);                           // Y = L_K J
+    launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s);  // Y2 = J Z^T J, Y = L_K J
     check_launch();
     launch_identity_lower(TL, np, lv, count, s);
     check_launch();

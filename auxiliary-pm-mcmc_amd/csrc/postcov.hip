@@ -51,77 +51,90 @@ void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Li
 }
 
 // Y2[a][k'] = W^1/2[np-1-k'] * L[np-1-k'][np-1-a] for k' <= a, 0 above (all np x np of dst from
-// column dcol0), where L is the lower factor held in `src`. Lower tile (ta, tk') of dst is the
-// reversed transpose of the source tile (nb-1-tk', nb-1-ta), staged through LDS.
-__global__ __launch_bounds__(256) void k_form_y2(MatB src, MatB dst, int64_t dcol0,
-                                                 const double* __restrict__ Ws, int64_t vstride,
-                                                 int nb, Live live) {
-    const int b = blockIdx.y;
-    if (!live_pc(live, b)) return;
-    const int ta = blockIdx.x / nb, tk = blockIdx.x % nb;
-    const int np = nb * 64;
-    double* D = dst.base + b * dst.cstride + (int64_t)(ta * 64) * dst.ld + dcol0 + tk * 64;
-    // 16-byte pieces: thread t, step h handles row (t + 256h) / 32, columns 2 ((t + 256h) % 32) .. +1
-    if (tk > ta) {  // upper tiles are read as zeros by the SYRK's panel-wide k-range
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            const int e = threadIdx.x + 256 * h;
-            *reinterpret_cast<d2_t*>(D + (int64_t)(e >> 5) * dst.ld + 2 * (e & 31)) = d2_t{0.0, 0.0};
-        }
-        return;
-    }
-    const int sr = nb - 1 - tk, sc = nb - 1 - ta;  // source tile (lower: sr >= sc)
-    __shared__ double T[64][65];
-    const double* S = src.base + b * src.cstride + (int64_t)(sr * 64) * src.ld + sc * 64;
-    d2_t v[8];
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        const int e = threadIdx.x + 256 * h;
-        v[h] = *reinterpret_cast<const d2_t*>(S + (int64_t)(e >> 5) * src.ld + 2 * (e & 31));
-    }
+// column dcol0): lower tile (ta, tk') of dst is the reversed transpose of the source tile
+// (nb-1-tk', nb-1-ta), staged through LDS. In the same pass L is overwritten in place by
+// Y = L J (L's lower triangle only, the rest read as zero). Workgroup (sr, c1), c1 <= c2 = nb-1-c1,
+// holds P = L(sr, c1) and Q = L(sr, c2), writes their Y2 tiles into dst and the column-reversed
+// tiles Y(sr, c2) = rev(P), Y(sr, c1) = rev(Q) back into L; every load is consumed into LDS ahead
+// of a barrier before any thread writes L. One read of L's lower triangle in all.
+__device__ __forceinline__ void load_lower_tile(const double* Lr, int64_t ld, int sr, int sc,
+                                                d2_t v[8]) {
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
         const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
-        T[r][c] = (sr > sc || c <= r) ? v[h].x : 0.0;
-        T[r][c + 1] = (sr > sc || c + 1 <= r) ? v[h].y : 0.0;
+        d2_t x = d2_t{0.0, 0.0};
+        if (sc <= sr) x = *reinterpret_cast<const d2_t*>(Lr + (int64_t)r * ld + sc * 64 + c);
+        v[h] = d2_t{(sr > sc || c <= r) ? x.x : 0.0, (sr > sc || c + 1 <= r) ? x.y : 0.0};
+    }
+}
+
+// Y2 tile of source tile (sr, sc) (as k_form_y2); T must be free on entry
+__device__ __forceinline__ void y2_tile(double (*T)[65], const d2_t v[8], int sr, int sc,
+                                        double* dbase, int64_t ld, int64_t dcol0,
+                                        const double* w, int nb) {
+    const int ta = nb - 1 - sc, tk = nb - 1 - sr, np = nb * 64;
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
+        T[r][c] = v[h].x;
+        T[r][c + 1] = v[h].y;
     }
     __syncthreads();
-    const double* w = Ws + b * vstride;
+    double* D = dbase + (int64_t)(ta * 64) * ld + dcol0 + tk * 64;
+    if (tk > ta) {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const int e = threadIdx.x + 256 * h;
+            *reinterpret_cast<d2_t*>(D + (int64_t)(e >> 5) * ld + 2 * (e & 31)) = d2_t{0.0, 0.0};
+        }
+        return;
+    }
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
         const int e = threadIdx.x + 256 * h;
-        const int al = e >> 5, kl = 2 * (e & 31);  // local output row (a) and columns (k', k'+1)
+        const int al = e >> 5, kl = 2 * (e & 31);
         const int kg = tk * 64 + kl;
-        *reinterpret_cast<d2_t*>(D + (int64_t)al * dst.ld + kl) =
+        *reinterpret_cast<d2_t*>(D + (int64_t)al * ld + kl) =
             d2_t{w[np - 1 - kg] * T[63 - kl][63 - al], w[np - 2 - kg] * T[62 - kl][63 - al]};
     }
 }
 
-void launch_form_y2(MatB src, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride, int np,
-                    Live live, int nchains, hipStream_t s) {
-    const int nb = np / 64;
-    hipLaunchKernelGGL(k_form_y2, dim3(nb * nb, nchains), dim3(256), 0, s, src, dst,
-                       dcol0, Ws, vstride, nb, live);
-}
-
-// in place: Y = L J restricted to L's lower triangle (the rest of L is treated as zero)
-__global__ __launch_bounds__(256) void k_reverse_cols(MatB M, int np, Live live) {
+__global__ __launch_bounds__(256) void k_form_y2_rev(MatB L, MatB dst, int64_t dcol0,
+                                                     const double* __restrict__ Ws,
+                                                     int64_t vstride, int nb, Live live) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int half = np / 2;
-    if (e >= (int64_t)np * half) return;
-    const int i = (int)(e / half), c = (int)(e % half), c2 = np - 1 - c;
-    double* row = M.base + b * M.cstride + (int64_t)i * M.ld;
-    const double l1 = (c <= i) ? row[c] : 0.0, l2 = (c2 <= i) ? row[c2] : 0.0;
-    row[c] = l2;
-    row[c2] = l1;
+    const int half = (nb + 1) / 2;
+    const int sr = blockIdx.x / half, c1 = blockIdx.x % half, c2 = nb - 1 - c1;
+    double* Lr = L.base + b * L.cstride + (int64_t)(sr * 64) * L.ld;
+    double* dbase = dst.base + b * dst.cstride;
+    const double* w = Ws + b * vstride;
+    __shared__ double T[64][65];
+    d2_t p[8], q[8];
+    load_lower_tile(Lr, L.ld, sr, c1, p);
+    if (c2 != c1) load_lower_tile(Lr, L.ld, sr, c2, q);
+    y2_tile(T, p, sr, c1, dbase, dst.ld, dcol0, w, nb);
+    __syncthreads();
+    if (c2 != c1) {
+        y2_tile(T, q, sr, c2, dbase, dst.ld, dcol0, w, nb);
+    } else {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) q[h] = p[h];
+    }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h, r = e >> 5, k = e & 31;
+        double* row = Lr + (int64_t)r * L.ld + 2 * (31 - k);
+        *reinterpret_cast<d2_t*>(row + c1 * 64) = d2_t{q[h].y, q[h].x};
+        *reinterpret_cast<d2_t*>(row + c2 * 64) = d2_t{p[h].y, p[h].x};
+    }
 }
 
-void launch_reverse_cols(MatB M, int np, Live live, int nchains, hipStream_t s) {
-    const int64_t tot = (int64_t)np * (np / 2);
-    hipLaunchKernelGGL(k_reverse_cols, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0,
-                       s, M, np, live);
+void launch_form_y2_rev(MatB L, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride,
+                        int np, Live live, int nchains, hipStream_t s) {
+    const int nb = np / 64;
+    hipLaunchKernelGGL(k_form_y2_rev, dim3(nb * ((nb + 1) / 2), nchains), dim3(256), 0, s, L, dst,
+                       dcol0, Ws, vstride, nb, live);
 }
 
 // lower tiles of M <- I
