@@ -52,7 +52,8 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
                         Live live, int nchains, hipStream_t s,
                         FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 // the same with one 128x128 super-tile per workgroup (tiles from build_update_supertiles)
-void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+// plus: 0 A -= ..., 1 A += ..., 2 A = I + ... (the old tile is not read)
+void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int plus,
                              Live live, int nchains, hipStream_t s,
                              FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 long update_tile_count(int i0, int R, int j0, int jend);

@@ -225,7 +225,7 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
 std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g);
 
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
-                    bool plus, int count, int fuse_k = -1, int fail_code = 0,
+                    int plus, int count, int fuse_k = -1, int fail_code = 0,
                     const Exec* ex = nullptr) {
     const Exec E = ex ? *ex : main_exec(c);
     if (i0 < j0) i0 = j0;
@@ -241,7 +241,8 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
         const auto sl = super_list(c, i0, R, j0, jend, g);
         launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd);
     } else {
-        launch_chol_update(M, k0, kc, tl.first, tl.second, plus, E.lv, count, E.s, fd);
+        if (plus == 2) throw HipError{"identity-initialised update needs the t128 path"};
+        launch_chol_update(M, k0, kc, tl.first, tl.second, plus != 0, E.lv, count, E.s, fd);
     }
     check_launch();
 }
@@ -680,11 +681,17 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     }
     launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s);  // Y2 = J Z^T J, Y = L_K J
     check_launch();
-    launch_identity_lower(TL, np, lv, count, s);
-    check_launch();
+    // the first panel's update writes I + Y2 Y2^T without reading TL when it takes the 128x128
+    // super-tile path (every lower tile of TL is in its range); otherwise TL starts as I
+    const bool init = (c->t128 & 2) && nb >= 2 && std::min(OUTER, nb) >= 2;
+    if (!init) {
+        launch_identity_lower(TL, np, lv, count, s);
+        check_launch();
+    }
     for (int K = 0; K < nb; K += OUTER) {  // J M J = I + Y2 Y2^T (Y2 lower: j >= K suffices)
         const int Kend = std::min(K + OUTER, nb);
-        tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, true, count);
+        tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, (init && K == 0) ? 2 : 1,
+                       count);
     }
     chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
     launch_trmv_tiles(true, TL, c->v.z, c->v.Kb, vs, np, c->sympart, c->sstride, lv, count,

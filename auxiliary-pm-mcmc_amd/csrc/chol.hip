@@ -379,7 +379,7 @@ struct __attribute__((aligned(16))) GemmSmem64T {
     double b[2][128][KS64T];
 };
 
-template <bool NEG>
+template <bool NEG, bool INIT = false>
 __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigned e, int b,
                                                  bool fused, Live live, FusedDiag<double> fd,
                                                  GemmSmem64T& smg, DiagSmem& smd) {
@@ -454,6 +454,12 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
         for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+                if (INIT) {  // old tile = I (plus == 2): nothing to read
+                    acc[bi][bj][r] =
+                        (li * 64 + 16 * bi + F64_CROW(lane, r) == lj * 64 + 16 * bj + r16) ? 1.0
+                                                                                          : 0.0;
+                    continue;
+                }
                 const double v = Cw[(int64_t)(16 * bi + F64_CROW(lane, r)) * A.ld + 16 * bj + r16];
                 acc[bi][bj][r] = NEG ? -v : v;
             }
@@ -534,18 +540,20 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_t128(MatB A, int k0, int
         t = (int)(w % nt) + (fd.enabled ? 1 : 0);
     }
     if (!chain_live(live, b)) return;
-    if (plus)  // A_ij += ... (the SYRK of the UL factorisation, postcov.hip)
+    if (plus == 2)  // A_ij = I_ij + ... (first SYRK panel of the UL factorisation, postcov.hip)
+        update_t128_body<false, true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+    else if (plus)  // A_ij += ...
         update_t128_body<false>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
     else
         update_t128_body<true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
 }
 
-void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, bool plus,
+void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int plus,
                              Live live, int nchains, hipStream_t s, FusedDiag<double> fd) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update_t128, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc,
-                       tiles, ntiles, nchains, (int)plus, live, fd);
+                       tiles, ntiles, nchains, plus, live, fd);
 }
 
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
