@@ -52,7 +52,8 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
                         Live live, int nchains, hipStream_t s,
                         FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 // the same with one 128x128 super-tile per workgroup (tiles from build_update_supertiles)
-// plus: 0 A -= ..., 1 A += ..., 2 A = I + ... (the old tile is not read)
+// plus: 0 A -= ..., 1 A += ..., 2 A = I + Y Y^T for lower-triangular Y (depth per tile column
+// truncated to the nonzero blocks; the old tile is not read)
 void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int plus,
                              Live live, int nchains, hipStream_t s,
                              FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});

@@ -196,13 +196,15 @@ Gap no_gap(int, int) { return Gap{0, 0}; }
 // tile k < nb-1-I, so at column k only bottom rows >= 2nb-1-k are nonzero.
 Gap y_gap(int k, int nb) { return Gap{nb, std::max(nb, 2 * nb - 1 - k)}; }
 
-double update_flops(int i0, int R, int j0, int jend, int kc, Gap g) {
+double update_flops(int i0, int R, int j0, int jend, int kc, Gap g, bool syrk_lower = false) {
     double f = 0.0;
     for (int i = i0; i < R; ++i) {
         if (i >= g.lo && i < g.hi) continue;
         const int jmax = std::min(i, jend - 1);
-        for (int j = j0; j <= jmax; ++j)
-            f += (i == j) ? 64.0 * 65.0 * 64.0 * kc : 2.0 * 64.0 * 64.0 * 64.0 * kc;
+        for (int j = j0; j <= jmax; ++j) {
+            const int k = syrk_lower ? std::min(kc, j + 1) : kc;  // plus == 2: k <= j only
+            f += (i == j) ? 64.0 * 65.0 * 64.0 * k : 2.0 * 64.0 * 64.0 * 64.0 * k;
+        }
     }
     return f;
 }
@@ -234,7 +236,7 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     if (tl.second <= 0) return;
     FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0) fd = FusedDiag<double>{1, E.Dinv, c->dstride, E.ldet, c->lstride, fail_code};
-    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g) * count : 0.0;
+    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g, plus == 2) * count : 0.0;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl, E.s);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
     if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
@@ -681,17 +683,18 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     }
     launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s);  // Y2 = J Z^T J, Y = L_K J
     check_launch();
-    // the first panel's update writes I + Y2 Y2^T without reading TL when it takes the 128x128
-    // super-tile path (every lower tile of TL is in its range); otherwise TL starts as I
-    const bool init = (c->t128 & 2) && nb >= 2 && std::min(OUTER, nb) >= 2;
-    if (!init) {
+    // J M J = I + Y2 Y2^T: on the 128x128 super-tile path one launch writes it without reading TL
+    // (tile column j takes Y2's column blocks k <= j); otherwise TL starts as I and receives
+    // panel-wide updates (Y2 lower: j >= K suffices)
+    if ((c->t128 & 2) && nb >= 2) {
+        tracked_update(c, TL, nb, nb, 0, nb, 0, nb, Gap{0, 0}, 2, count);
+    } else {
         launch_identity_lower(TL, np, lv, count, s);
         check_launch();
-    }
-    for (int K = 0; K < nb; K += OUTER) {  // J M J = I + Y2 Y2^T (Y2 lower: j >= K suffices)
-        const int Kend = std::min(K + OUTER, nb);
-        tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, (init && K == 0) ? 2 : 1,
-                       count);
+        for (int K = 0; K < nb; K += OUTER) {
+            const int Kend = std::min(K + OUTER, nb);
+            tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, 1, count);
+        }
     }
     chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
     launch_trmv_tiles(true, TL, c->v.z, c->v.Kb, vs, np, c->sympart, c->sstride, lv, count,

@@ -443,7 +443,9 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
 #endif
         }
     };
-    const int nsub = (64 * kc) / KS64T;
+    // INIT (the SYRK I + Y Y^T, Y lower triangular from column block k0): block k of Y is zero in
+    // rows above it, so tiles of column j need k <= j only - one launch over the whole depth
+    const int nsub = (64 * (INIT ? min(kc, max(cb0, cb1) + 1) : kc)) / KS64T;
     // old tile into acc (negated for A_ij -= ...: acc = -C + sum, result = -acc), consumed before
     // the loop so that no wait for it lands inside (see k_chol_update32_t128)
     const int li = mine ? oi : (wr ? ra1 : ra0), lj = mine ? oj : (wc ? cb1 : cb0);
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_t128(MatB A, int k0, int
         t = (int)(w % nt) + (fd.enabled ? 1 : 0);
     }
     if (!chain_live(live, b)) return;
-    if (plus == 2)  // A_ij = I_ij + ... (first SYRK panel of the UL factorisation, postcov.hip)
+    if (plus == 2)  // A_ij = I_ij + Y_i Y_j^T (the SYRK of the UL factorisation, postcov.hip)
         update_t128_body<false, true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
     else if (plus)  // A_ij += ...
         update_t128_body<false>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
