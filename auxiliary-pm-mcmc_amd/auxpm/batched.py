@@ -32,9 +32,20 @@ import numpy as np
 from gpdemo import _native
 from gpdemo.utils import log_prior_ard_batch
 
-__all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler']
+__all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler', 'chain_streams']
 
 _EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC}
+
+
+def chain_streams(seed, n_chains):
+    """Per-chain random streams of a batch: numpy.random.SeedSequence(seed).spawn(n_chains)
+    gives each chain a host RandomState (MT19937; slice heights, angles, directions, MH draws)
+    and a 64-bit Philox4x32-10 key for its device draws (u, nu). Different `seed`s (bench.py
+    derives one per rank) give statistically independent, non-overlapping streams."""
+    kids = np.random.SeedSequence(seed).spawn(n_chains)
+    prngs = [np.random.RandomState(np.random.MT19937(k)) for k in kids]
+    dev_seeds = np.array([k.generate_state(2, np.uint64)[0] for k in kids], dtype=np.uint64)
+    return prngs, dev_seeds
 
 
 class BatchedAPMEllSSPlusRandDirSliceSampler(object):
@@ -64,11 +75,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.ub_u = np.arange(C, dtype=np.int64)
         self.ub_nu = np.arange(C, 2 * C, dtype=np.int64)
         self.ub_prop = np.arange(2 * C, 3 * C, dtype=np.int64)
-        ss = np.random.SeedSequence(seed)
-        kids = ss.spawn(C)
-        self.prngs = [np.random.RandomState(np.random.MT19937(k)) for k in kids]
-        self.dev_seeds = np.array([k.generate_state(2, np.uint64)[0] for k in kids],
-                                  dtype=np.uint64)
+        self.prngs, self.dev_seeds = chain_streams(seed, C)
         self.dev_ctr = np.zeros(C, dtype=np.uint64)
         self.theta = np.zeros((C, self.P))
         self.log_f = np.full(C, -np.inf)

@@ -77,13 +77,14 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
-                          int hlim = 0);
+                          int hlim = 0, const int* h3ok = nullptr);
 // the same update with one 128x128 super-tile per workgroup (tiles from build_update_supertiles);
-// hlim > 0: fp16x3 operands (chol32.hip) for super-tiles whose rows lie below row tile hlim
+// hlim > 0: fp16x3 operands (chol32.hip) for super-tiles whose rows lie below row tile hlim, in
+// the chains b with h3ok[b] != 0 (h3ok == nullptr: every chain); the others take fp32 operands
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
-                               int hlim = 0);
+                               int hlim = 0, const int* h3ok = nullptr);
 std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi);
 // y = K x from K's lower tiles (part: nb*nb*64 doubles per chain of partials); Bf.base != null
 // also forms the fp32 Newton matrix I + W^1/2 K W^1/2 and its right-hand-side block (x = b)

@@ -59,6 +59,7 @@ struct apm_ctx {
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;  // d_ubufs = d_slots + B
     // pinned host staging of the per-call transfers (one H2D of slots + ubufs, D2H copies that
     // are enqueued together and waited on once): [B slots][B ubufs][B out][B status][B n_iter]
+    // [B h3ok]
     char* hpin = nullptr;
     int64_t* hblk = nullptr;  // pinned mirror of the d_i3 .. d_ctrs block (apm_u_normal/combine)
     double* hth = nullptr;    // pinned theta staging (B x P)
@@ -83,7 +84,11 @@ struct apm_ctx {
     bool trsv_fused = true;
     bool trsv_mw = true;  // APM_TRSV_MW=0: one workgroup per chain (k_trsv32_fused)
     bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
-    bool h3_now = false;  // fp16x3 allowed for the current theta-call (range check on theta_0)
+    bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
+    int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
+    // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
+    // previous convergence read; update_flops x live_n instead of x count)
+    int live_n = 0;
     // chol(K) of the IS theta-call on a low-priority second stream, concurrent with the Newton
     // iterations (APM_OVERLAP_K=0: after them, on the main stream)
     bool overlap_k = true;
@@ -174,8 +179,9 @@ struct Exec {
     Live lv;
     double* Dinv;
     double* ldet;
+    int live_n;  // chains credited by the roofline accounting
 };
-Exec main_exec(apm_ctx* c) { return Exec{c->stream, live_of(c), c->Dinv, c->ldet}; }
+Exec main_exec(apm_ctx* c) { return Exec{c->stream, live_of(c), c->Dinv, c->ldet, c->live_n}; }
 
 // Two-level right-looking Cholesky over tile columns [k0, k1) of rows < R (tile units), the
 // trailing matrix spanning columns < Cb. Outer panels of OUTER tiles (256 columns) are factored
@@ -236,7 +242,7 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     if (tl.second <= 0) return;
     FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0) fd = FusedDiag<double>{1, E.Dinv, c->dstride, E.ldet, c->lstride, fail_code};
-    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g, plus == 2) * count : 0.0;
+    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g, plus == 2) * E.live_n : 0.0;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl, E.s);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
     if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
@@ -335,16 +341,16 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0)
         fd = FusedDiag<float>{1, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, fail_code};
-    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * count : 0.0;
+    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl);
     if ((c->t128 & 1) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0});
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  fd, c->h3_now ? c->nb : 0);
+                                  fd, c->h3_now ? c->nb : 0, c->h3ok);
     } else {
         launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd,
-                             c->h3_now ? c->nb : 0);
+                             c->h3_now ? c->nb : 0, c->h3ok);
     }
     check_launch();
 }
@@ -410,6 +416,16 @@ void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubuf
 double* pin_out(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 16 * c->max_batch); }
 int* pin_status(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 32 * c->max_batch); }
 int* pin_iter(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 36 * c->max_batch); }
+int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 40 * c->max_batch); }
+
+// per-chain fp16x3 flags of a theta-call -> device (chol32.hip: |L_ij| <= sqrt(1 + K_ii) must
+// stay below fp16's range); h3_now = any chain flagged (else the fp32-operand kernel launches)
+void upload_h3(apm_ctx* c, int count) {
+    int* h = pin_h3(c);
+    c->h3_now = false;
+    for (int b = 0; b < count; ++b) c->h3_now |= h[b] != 0;
+    HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
+}
 
 void u_eval_device(apm_ctx* c, int count) {
     {
@@ -511,8 +527,9 @@ void newton_solve32(apm_ctx* c, int count) {
     }
 }
 
-void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
+void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0) {
     const Live lv = live_of(c);
+    c->live_n = live0;
     // f = 0 for the live chains only (a fallback rerun must keep the other chains' modes)
     launch_refine(3, nullptr, nullptr, nullptr, nullptr, c->v.f, c->v.vstride, c->np, lv, count,
                   c->stream);
@@ -562,9 +579,10 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
         sync(c);
         std::memcpy(act.data(), pin_iter(c), sizeof(int) * count);
         std::memcpy(st_h.data(), pin_status(c), sizeof(int) * count);
-        bool any = false;
-        for (int b = 0; b < count; ++b) any |= (act[b] != 0 && st_h[b] == 0);
-        if (!any) break;
+        int live = 0;
+        for (int b = 0; b < count; ++b) live += (act[b] != 0 && st_h[b] == 0);
+        if (!live) break;
+        c->live_n = live;
     }
     bool changed = false;
     for (int b = 0; b < count; ++b)
@@ -579,8 +597,10 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed) {
 
 // Newton for the IS estimator: mixed precision, with an fp64 rerun for any chain whose fp32
 // factorisation broke down (B is SPD with eigenvalues >= 1, so only for extreme theta)
+void drain_chol_k(apm_ctx* c);
+
 void newton_is(apm_ctx* c, int count, std::vector<int>& st_h) {
-    newton(c, count, st_h, c->mixed);
+    newton(c, count, st_h, c->mixed, count);
     if (!c->mixed) return;
     std::vector<int> redo;
     for (int b = 0; b < count; ++b)
@@ -599,8 +619,12 @@ void newton_is(apm_ctx* c, int count, std::vector<int>& st_h) {
                         c->stream));
     HIPC(hipMemcpyAsync(c->n_iter, nit.data(), sizeof(int) * count, hipMemcpyHostToDevice,
                         c->stream));
+    // The fp64 rerun forms B and its right-hand-side row in A's rows [0, np]; row block np is
+    // the first row block of BL, which the concurrent chol(K) on stream2 may still be writing:
+    // let chol(K) finish first (L_K is recomputed after the rerun anyway, theta_eval_impl)
+    drain_chol_k(c);
     // only the redo chains are live now: converged chains have active = 0, failed ones status != 0
-    newton(c, count, st_h, false);
+    newton(c, count, st_h, false, (int)redo.size());
 }
 
 void augmented(apm_ctx* c, int count, bool factor_C) {
@@ -655,8 +679,18 @@ void chol_k_into_bl(apm_ctx* c, int count, const Exec& ex) {
     c->cholk_next = -1;
 }
 
+// enqueue what is left of the concurrent chol(K) and order the main stream behind it
+void drain_chol_k(apm_ctx* c) {
+    if (c->cholk_next < 0) return;
+    while (c->cholk_next < c->nb) chol_k_panel(c, k_exec(c, c->stream2));
+    c->cholk_next = -1;
+    HIPC(hipEventRecord(c->ev_cholk, c->stream2));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
+}
+
 Exec k_exec(apm_ctx* c, hipStream_t s) {
-    return Exec{s, Live{c->active2, c->status2}, c->Dinv + (int64_t)c->nb * 4096, c->ldet + c->nb};
+    return Exec{s, Live{c->active2, c->status2}, c->Dinv + (int64_t)c->nb * 4096, c->ldet + c->nb,
+                c->cholk_count};
 }
 
 // L_K ready in BL (chol_k_into_bl); h = L_K^-1 f_post = L_K^T a because f_post = K a
@@ -705,6 +739,7 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
 void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf, int* status,
                      int64_t* nops) {
     const Live lv = live_of(c);
+    c->live_n = count;
     HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
     HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
@@ -734,15 +769,13 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         }
         const int64_t reruns = c->n_fp64_rerun;
         if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself
-            newton(c, count, st_h, false);
+            newton(c, count, st_h, false, count);
         else
             newton_is(c, count, st_h);
+        c->live_n = 0;
+        for (int b = 0; b < count; ++b) c->live_n += st_h[b] == 0;
         if (ov) {
-            while (c->cholk_next >= 0 && c->cholk_next < c->nb)  // what the TRSVs did not take
-                chol_k_panel(c, k_exec(c, c->stream2));
-            c->cholk_next = -1;
-            HIPC(hipEventRecord(c->ev_cholk, c->stream2));
-            HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
+            drain_chol_k(c);  // what the TRSVs did not take (a no-op after an fp64 rerun)
             if (c->n_fp64_rerun != reruns)  // the fp64 Newton rerun used rows of BL: redo L_K
                 chol_k_into_bl(c, count, k_exec(c, c->stream));
             launch_merge_status(c->status, c->status2, APM_STATUS_CHOL_K, count, c->stream);
@@ -885,7 +918,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 40, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 44, hipHostMallocDefault));
+    c->h3ok = dalloc<int>(c, B);
     // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:
     // [i3: 3B int64][ca: B][cb: B][seeds: B][ctrs: B]
     c->d_i3 = dalloc<int64_t>(c, 7 * B);
@@ -1084,9 +1118,9 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
             for (int p = 0; p < c->P; ++p) th[b * c->P + p] = thetas[b * ldt + p];
         HIPC(hipMemcpyAsync(c->theta, th, sizeof(double) * count * c->P, hipMemcpyHostToDevice,
                             c->stream));
-        // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip)
-        c->h3_now = c->h3;
-        for (int64_t b = 0; b < count; ++b) c->h3_now &= th[b * c->P] < 19.0;
+        // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip): per chain
+        for (int64_t b = 0; b < count; ++b) pin_h3(c)[b] = c->h3 && th[b * c->P] < 19.0;
+        upload_h3(c, (int)count);
         if (est != APM_EST_LAPLACE) upload_idx(c, (int)count, slots, ubufs);
         theta_eval_impl(c, est, (int)count, true, out_logf, status, nops);
     } catch (const HipError& e) {
@@ -1114,7 +1148,8 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
                             hipMemcpyHostToDevice, c->stream));
         double kmax = 0.0;
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
-        c->h3_now = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
+        pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
+        upload_h3(c, 1);
         HIPC(hipMemcpyAsync(c->d_slots, &slot, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
         HIPC(hipMemcpyAsync(c->d_ubufs, &ubuf, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);
@@ -1255,7 +1290,8 @@ int apm_laplace(int device, const double* K, int64_t n, int64_t ldk, const doubl
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
         HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int), c->stream));
         std::vector<int> st(1, 0);
-        newton(c, 1, st, false);
+        c->live_n = 1;
+        newton(c, 1, st, false, 1);
         int it = 0;
         HIPC(hipMemcpyAsync(&it, c->n_iter, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         sync(c);

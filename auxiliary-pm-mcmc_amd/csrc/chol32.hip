@@ -236,7 +236,8 @@ __device__ __forceinline__ long xcd_remap32(long L, long total) {
 __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
                                                        const unsigned* __restrict__ tiles,
                                                        int ntiles, int nchains, Live live,
-                                                       FusedDiag<float> fd, int hlim) {
+                                                       FusedDiag<float> fd, int hlim,
+                                                       const int* __restrict__ h3ok) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -264,7 +265,8 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-    if (i < hlim)  // fp16x3 below the appended right-hand-side row tile (k_chol_update32_t128)
+    // fp16x3 below the appended right-hand-side row tile, per chain (k_chol_update32_t128)
+    if (i < hlim && (!h3ok || h3ok[b]))
         tile_gemm_nt32<true, true>(acc, Ab + (int64_t)(i * 64) * A.ld + k0 * 64, A.ld,
                                    Ab + (int64_t)(j * 64) * A.ld + k0 * 64, A.ld, 64 * kc, sm.g,
                                    Aij, A.ld);
@@ -299,11 +301,12 @@ __global__ __launch_bounds__(256) void k_chol_update32(MatF A, int k0, int kc,
 }
 
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
-                          int nchains, hipStream_t s, FusedDiag<float> fd, int hlim) {
+                          int nchains, hipStream_t s, FusedDiag<float> fd, int hlim,
+                          const int* h3ok) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
-                       ntiles, nchains, live, fd, hlim);
+                       ntiles, nchains, live, fd, hlim, h3ok);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -336,15 +339,17 @@ struct __attribute__((aligned(16))) GemmSmemH3 {
 // matrices (numpy emulation, N = 1024, sigma = 1 .. e^4) the factor's residual |LL^T - B| is
 // unchanged and the refinement contraction rises from ~3e-6 to ~1e-5, far below the 1e-3 of the
 // acceptance test. fp16's range bounds the operands (entries of L, |L_ij| <= sqrt(B_ii) <=
-// sqrt(B_ii) = sqrt(1 + W_i K_ii) <= sqrt(1 + e^theta_0 + eps), probit W < 1): the host enables
-// it only while every chain of the launch has theta_0 < 19 (entries < 1.4e4 < 65504). The
-// appended right-hand-side row (forward solve of W^1/2 K b, unbounded) stays fp32: super-tiles
-// reaching row tile hlim take the fp32 path.
+// sqrt(B_ii) = sqrt(1 + W_i K_ii) <= sqrt(1 + e^theta_0 + eps), probit W < 1): the host flags
+// the chains with theta_0 < 19 (entries < 1.4e4 < 65504) in h3ok; the others take the fp32
+// path inside the same launch, so a chain's result does not depend on its batch. The appended
+// right-hand-side row (forward solve of W^1/2 K b, unbounded) stays fp32: super-tiles reaching
+// row tile hlim take the fp32 path.
 template <bool H3>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
-                                                               FusedDiag<float> fd, int hlim) {
+                                                               FusedDiag<float> fd, int hlim,
+                                                               const int* __restrict__ h3ok) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     __shared__ union {
@@ -387,7 +392,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 acc[bi][bj][r] = -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
-    if (H3 && ti + 1 < hlim) {  // super-tile rows below hlim (the appended right-hand side row)
+    // super-tile rows below hlim (the appended right-hand side row), chains flagged in h3ok
+    if (H3 && ti + 1 < hlim && (!h3ok || h3ok[b])) {
         // register staging: thread tid moves 16-byte pieces p = tid + 256h (row p/8, k 4(p%8))
         // of both operands
         const float* arow[4];
@@ -573,15 +579,15 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
-                               int hlim) {
+                               int hlim, const int* h3ok) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     if (hlim > 0)
         hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, hlim);
+                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok);
     else
         hipLaunchKernelGGL(k_chol_update32_t128<false>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, 0);
+                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr);
 }
 
 // Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),

@@ -55,29 +55,25 @@ def parse():
 
 
 class Dist(object):
-    """One process per GPU. torch.distributed only for the barrier and the max/sum reductions of
-    the timing (RCCL on GPUs, gloo for CPU tests); the chains never exchange data."""
+    """One process per GPU. torch.distributed (gloo, on the host) only for the barrier and the
+    max/sum reductions of the timing; the chains never exchange data, so no RCCL communicator is
+    created (north_star: "no RCCL required" - one failure mode fewer on an 8-GPU node)."""
 
-    def __init__(self, backend=None):
+    def __init__(self, backend='gloo'):
         self.world = int(os.environ.get('WORLD_SIZE', '1'))
         self.rank = int(os.environ.get('RANK', '0'))
         self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
         self.dist = None
+        self.backend = None
         if self.world > 1:
-            import torch
             import torch.distributed as dist
-            if backend is None:
-                backend = 'nccl' if torch.cuda.is_available() else 'gloo'
-            if backend == 'nccl':
-                torch.cuda.set_device(self.local_rank)
             dist.init_process_group(backend=backend)
             self.dist = dist
             self.backend = backend
 
     def _t(self, x):
         import torch
-        dev = 'cuda' if self.backend == 'nccl' else 'cpu'
-        return torch.tensor([float(x)], dtype=torch.float64, device=dev)
+        return torch.tensor([float(x)], dtype=torch.float64)
 
     def barrier(self):
         if self.dist is not None:
@@ -100,6 +96,12 @@ class Dist(object):
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
+
+
+def chain_seed(base, rank):
+    """Seed of rank `rank`'s sampler. Each rank's SeedSequence(seed) spawns its chains' host and
+    device (Philox) streams; distinct rank seeds give disjoint chain streams (test_bench_dist)."""
+    return base + 7919 * rank
 
 
 def device_sync():
@@ -150,24 +152,34 @@ def timed_region(dist, step_fn, steps, on_start=None):
     return dist.max(time.perf_counter() - t0)
 
 
-def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget):
-    """Time the CPU restatement (oracle/: C Gram + scipy LAPACK, the reference's op order) on a
-    bounded sample: theta-calls and cached u-calls at the benchmark size, composed into
-    transitions/s with the per-transition call counts measured on the GPU run."""
-    sys.path.insert(0, os.path.join(REPO, 'oracle'))
-    import apm_oracle as orc
+def _blas_threads():
     try:
         from threadpoolctl import threadpool_info
-        blas_threads = max([i.get('num_threads', 1) for i in threadpool_info()
-                            if i.get('user_api') == 'blas'] or [1])
+        return max([i.get('num_threads', 1) for i in threadpool_info()
+                    if i.get('user_api') == 'blas'] or [1])
     except Exception:
-        blas_threads = None
+        return None
+
+
+def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, min_theta_calls=3):
+    """Time the CPU restatement (oracle/: C Gram + scipy LAPACK, the reference's op order) on a
+    bounded sample: >= 3 theta-calls and cached u-calls at the benchmark size, composed into
+    transitions/s of ONE chain with the per-transition call counts measured on the GPU run; plus
+    configs[0] (PM-MH, iso kernel, N=768 D=8, N_imp=1: one theta-call per MH iteration), the
+    reference's own CPU configuration. The port/reference calibration ratio measured in the
+    build container (tools/cpu_calibration.py -> profiles/r*_cpu_calibration.json) is attached."""
+    import glob
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import apm_oracle as orc
+    from gpdemo.utils import synthetic_gp_data
+    blas_threads = _blas_threads()
     est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
     rng = np.random.RandomState(0)
     ns = rng.normal(size=(X.shape[0], n_imp))
     t_theta, t_u = [], []
     t_start = time.perf_counter()
-    while True:
+    while len(t_theta) < min_theta_calls or (time.perf_counter() - t_start < budget
+                                             and len(t_theta) < 8):
         t0 = time.perf_counter()
         _, cache = est(ns, theta)
         t1 = time.perf_counter()
@@ -175,27 +187,52 @@ def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget):
         t2 = time.perf_counter()
         t_theta.append(t1 - t0)
         t_u.append(t2 - t1)
-        if time.perf_counter() - t_start > 0.5 * budget or len(t_theta) >= 5:
-            break
     tt, tu = float(np.median(t_theta)), float(np.median(t_u))
     per_transition = calls_theta * tt + calls_u * tu
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    # configs[0]: PM-MH iso N=768 D=8 N_imp=1 (Pseudo-Marginal MH.ipynb protocol)
+    X1, y1 = synthetic_gp_data(768, 8, 20151009, 'iso')
+    est1 = orc.ISEstimatorCPU(X1, y1, orc.make_kernel_func('iso', 1e-8, impl='c'))
+    th1 = np.r_[0.0, np.log(np.sqrt(8.))]
+    t_c1 = []
+    for r in range(5):
+        ns1 = np.random.RandomState(r).normal(size=(768, 1))
+        t0 = time.perf_counter()
+        est1(ns1, th1)
+        t_c1.append(time.perf_counter() - t0)
+    cores_visible = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') \
+        else os.cpu_count()
+    cal_files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_cpu_calibration.json')))
+    cal = json.load(open(cal_files[-1])) if cal_files else None
     return {
         'value': 1.0 / per_transition, 'unit': 'transitions/s (1 chain)',
-        'cores': blas_threads if blas_threads else cores, 'kind': 'port',
-        'sample': ('{0} theta-call(s) {1:.2f} s and cached u-call(s) {2:.3f} s (median) of the '
-                   'oracle ApproxPosteriorIS (C Gram 1 thread + scipy/OpenBLAS {3} threads, {4} '
-                   'cores visible) at N={5} D={6} N_imp={7}, composed with {8:.2f} theta-calls + '
-                   '{9:.2f} u-calls per transition measured on the GPU run'
-                   .format(len(t_theta), tt, tu, blas_threads, cores, X.shape[0], X.shape[1],
-                           n_imp, calls_theta, calls_u)),
-        'theta_call_s': tt, 'u_call_s': tu,
+        'cores': blas_threads if blas_threads else cores_visible, 'kind': 'port',
+        'cores_note': ('BLAS threads = the CPU share this process is given (OMP_NUM_THREADS={0}); '
+                       '{1} cores are visible to the process but belong to the whole host'
+                       .format(os.environ.get('OMP_NUM_THREADS', 'unset'), cores_visible)),
+        'sample': ('{0} theta-calls (median {1:.2f} s) and {0} cached u-calls (median {2:.3f} s) '
+                   'of the oracle ApproxPosteriorIS (C Gram 1 thread + scipy/OpenBLAS {3} '
+                   'threads) at N={4} D={5} N_imp={6}, composed with {7:.2f} theta-calls + '
+                   '{8:.2f} u-calls per transition measured on the GPU run'
+                   .format(len(t_theta), tt, tu, blas_threads, X.shape[0], X.shape[1], n_imp,
+                           calls_theta, calls_u)),
+        'theta_call_s': tt, 'u_call_s': tu, 'theta_calls_timed': len(t_theta),
+        'theta_call_s_all': t_theta,
+        'configs0_pmmh': {'iters_per_s': 1.0 / float(np.median(t_c1)),
+                          'sample': '5 theta-calls (fresh u each, as one PM-MH iteration) of the '
+                                    'oracle ApproxPosteriorIS, iso kernel, N=768 D=8 N_imp=1 '
+                                    '(Pima-shaped synthetic data)',
+                          'theta_call_s_median': float(np.median(t_c1))},
+        'calibration': cal,
     }
 
 
 def main():
     a = parse()
     dist = Dist()
+    if a.gpus != dist.world:
+        raise SystemExit('bench.py: --gpus {0} but WORLD_SIZE={1}; launch N>1 as `python -m '
+                         'torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr '
+                         '127.0.0.1 --master-port P bench.py --gpus N`'.format(a.gpus, dist.world))
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
     from auxpm.diagnostics import effective_size
     from gpdemo import _native
@@ -205,7 +242,7 @@ def main():
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
-        seed=a.seed + 7919 * dist.rank, device=dist.local_rank)
+        seed=chain_seed(a.seed, dist.rank), device=dist.local_rank)
     P = smp.P
     smp.initialise()
     if a.schedule == 'async':
@@ -234,7 +271,8 @@ def main():
             res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
         elapsed = timed_region(dist, body, 1, mark)
         done = res['done']
-        tr_list = [np.array(res['traces'][c][:a.steps]) for c in range(a.chains)
+        # every completed timed transition of each live chain (>= K per chain)
+        tr_list = [np.array(res['traces'][c]) for c in range(a.chains)
                    if not smp.failed[c] and done[c] >= a.steps]
     else:
         thetas = []
@@ -308,25 +346,43 @@ def main():
                                 'traffic': tr, 'traffic_source': src, 'launches': ucnt,
                                 'avg_launch_us': ums * 1e3 / ucnt,
                                 'algorithmic_flops_per_launch': uflops / ucnt}
-    ess_per_sec = None
-    if a.steps >= 100:  # min over theta components of each chain's ESS over its first K steps
-        ess = sum(effective_size(t).min() for t in tr_list)
-        ess_per_sec = dist.sum(ess) / elapsed
+    # ESS/s on theta (Analyse results.ipynb:138-139 uses coda's effectiveSize):
+    # sum over chains of min over theta components of the chain's ESS over ALL its completed
+    # timed transitions, / the timed wall time. Defined for any K (the driver runs K=20); with few
+    # transitions per chain after a short warm-up the AR(p) fit is noisy, so the sample is stated.
+    ess_c = [effective_size(t) for t in tr_list if len(t) >= 4]
+    n_per_chain = [len(t) for t in tr_list]
+    n_ess = dist.sum(len(ess_c))  # collectives on every rank, whatever its local sample
+    ess_min_sum = dist.sum(sum(e.min() for e in ess_c))
+    ess_mean_sum = dist.sum(sum(e.mean() for e in ess_c))
+    ess_per_sec = ess_min_sum / elapsed if n_ess else None
+    ess_mean_per_sec = ess_mean_sum / elapsed if n_ess else None
+    ess_first_k = None
+    if a.steps >= 100:  # the round-1 definition: each chain's first K timed transitions only
+        ess_first_k = dist.sum(sum(effective_size(t[:a.steps]).min() for t in tr_list)) / elapsed
+    ess_sample = {'chains': int(n_ess),
+                  'transitions_per_chain_min': int(-dist.max(-min(n_per_chain or [0]))),
+                  'transitions_per_chain_max': int(dist.max(max(n_per_chain or [0]))),
+                  'transitions_per_chain_mean': dist.sum(sum(n_per_chain)) /
+                  max(1., dist.sum(len(n_per_chain))),
+                  'warmup_transitions_discarded': a.warmup,
+                  'estimator': 'coda effectiveSize restatement (auxpm/diagnostics.py), per chain '
+                               'min over the {0} theta components, summed over chains'.format(P)}
 
     cpu = None
-    if a.cpu_baseline and dist.rank == 0 and dist.world == 1:
+    if a.cpu_baseline and dist.rank == 0:
         theta_ref = np.r_[0.0, np.full(a.d, np.log(np.sqrt(a.d)))]
         cpu = cpu_baseline(X, y, a.n_imp, theta_ref, n_th, n_u, a.cpu_budget)
-        cpu['value_same_chains'] = cpu['value'] * a.chains
         cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
 
     line = {
         'metric': METRIC, 'value': value, 'unit': 'transitions/s (all chains, all GPUs)',
         'n_gpus': dist.world, 'steps': a.steps, 'warmup': a.warmup,
         'ms_per_step': 1e3 * elapsed / a.steps, 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'f64',
+        'vs_baseline': None, 'dtype': 'mixed f64/f32',
         'dtype_detail': 'theta-path Gram, chol(K) and the posterior-covariance factor fp64 on f64 '
-                        'MFMA; Newton matrix B factored in fp32 (f32 MFMA) with fp64 iterative '
+                        'MFMA; Newton matrix B factored in fp32 (trailing updates fp16x3: fp16 '
+                        'hi/lo operand splits, fp32 accumulation; panels fp32) with fp64 iterative '
                         'refinement of each solve (mode = fp64 Newton mode to ~1e-12); '
                         'importance-sampling L.U fp32 on f32 MFMA; probit/LME epilogue fp32->fp64',
         'data': 'synthetic (X~N(0,1) normalised, y=sign of a GP prior draw; seed {0})'.format(a.seed),
@@ -337,7 +393,8 @@ def main():
                    'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
                    .format(dist.world)},
-        'ess_per_sec': ess_per_sec,
+        'ess_per_sec': ess_per_sec, 'ess_mean_per_sec': ess_mean_per_sec,
+        'ess_per_sec_first_k': ess_first_k, 'ess_sample': ess_sample,
         'schedule': a.schedule, 'transitions_timed': int(transitions),
         'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
         'failed_chains': int(dist.sum(int(smp.failed.sum()))),

@@ -240,6 +240,26 @@ def theta_state_reformulated(K, y):
                 n_ops=n_ops)
 
 
+def theta_state_pushthrough(K, y):
+    """The reformulated state with C_chol formed the way the device forms it (DESIGN.md §3.1
+    step 3, postcov.hip) instead of chol(K - V^T V) (estimators.py:206-209, lpa.py:111-112):
+    C = (K^-1 + W)^-1 = L_K M^-1 L_K^T with M = I + L_K^T W L_K (W of the last Newton iteration),
+    M = U U^T by the "UL" Cholesky (U = J chol(J M J) J upper, J the index reversal), so
+    C_chol = L_K U^-T (lower, positive diagonal) and log|B| = log|M|. M is SPD for any W >= 0,
+    so this never raises where the reference's chol(C) does (InvalidCovarianceMatrixError at
+    extreme theta, tests/golden/errors.npz icm_*); chol(K) failing still raises LinAlgError."""
+    K_chol = la.cholesky(K, lower=True)
+    f_post, _, n_ops, st = laplace_approximation(K, y, return_internals=True)
+    W = st['W_diag']
+    M = np.eye(K.shape[0]) + (K_chol.T * W[None]).dot(K_chol)
+    Lp = la.cholesky(M[::-1, ::-1], lower=True)
+    U = Lp[::-1, ::-1]                                   # upper, M = U U^T
+    C_chol = la.solve_triangular(U, K_chol.T, lower=False).T   # (U^-1 L_K^T)^T = L_K U^-T
+    g = la.solve_triangular(C_chol, f_post, lower=True)
+    logdet_M = 2. * np.log(Lp.diagonal()).sum()
+    return dict(C_chol=C_chol, f_post=f_post, W=W, g=g, logdet_B=logdet_M, n_ops=n_ops)
+
+
 def is_estimate_reformulated(y, state, ns):
     """IS log-estimate from the reformulated per-theta state (float64 statement of the GPU math)."""
     f_s = state['f_post'][:, None] + state['C_chol'].dot(ns)          # (N, S)

@@ -153,8 +153,33 @@ def error_fixture():
         verr = ''
     except ValueError as e:
         verr = str(e)
+    # extreme theta (iso, N=60 D=3): chol(K) fails -> numpy LinAlgError (estimators.py:206,
+    # uncaught), and the two thetas where chol(K) succeeds but chol(C) of C = K - V^T V fails ->
+    # InvalidCovarianceMatrixError (estimators.py:208-215), found by a grid search over
+    # log sigma in 6..16, log tau in 1..5
+    Xe, ye = synth_data(60, 3, 100, 'iso')
+    kf = kfunc('iso', 1e-8)
+    ns = np.random.RandomState(0).normal(size=(60, 4))
+    cases = {'cholk': np.array([20., 6.]), 'icm_a': np.array([15., 5.]),
+             'icm_b': np.array([16., 3.])}
+    out = {}
+    for name, th in cases.items():
+        est = ref_est.LogMarginalLikelihoodApproxPosteriorISEstimator(
+            Xe, ye, kf, ref_lpa.laplace_approximation)
+        try:
+            est(ns, th)
+            kind = 'none'
+            msg = ''
+        except ref_est.InvalidCovarianceMatrixError as e:
+            kind, msg = 'InvalidCovarianceMatrixError', str(e)
+        except np.linalg.LinAlgError as e:
+            kind, msg = 'LinAlgError', str(e)
+        out[name + '_theta'] = th
+        out[name + '_raised'] = np.array(kind)
+        out[name + '_msg'] = np.array(msg)
     np.savez_compressed(os.path.join(HERE, 'errors.npz'), X=X, y=y, K=K,
-                        laplace_maxiter_msg=np.array(raised), valueerror_msg=np.array(verr))
+                        laplace_maxiter_msg=np.array(raised), valueerror_msg=np.array(verr),
+                        extreme_X=Xe, extreme_y=ye, extreme_ns=ns, **out)
 
 
 # ----------------------------------------------------------------------------- sampler traces
@@ -335,6 +360,60 @@ def gp_chain_fixture():
     np.savez_compressed(os.path.join(HERE, 'gp_chain.npz'), **out)
 
 
+def pmmh_chain_fixture():
+    """BASELINE.json configs[0]: the PM-MH protocol of Pseudo-Marginal MH.ipynb (cells 12-14):
+    isotropic SE kernel, N_imp = 1, Laplace-estimator adaptive phase, then the ApproxPosteriorIS
+    main phase with fresh u from the shared prng at every proposal. Pima-shaped synthetic data
+    (N=768, D=8; the UCI file is not available), a shortened schedule (3 adaptive batches of 10,
+    30 main iterations). Records every estimator value in call order so the GPU replay can be
+    checked call by call."""
+    n, d, n_imp = 768, 8, 1
+    X, y = synth_data(n, d, 20151009, 'iso')
+    prior = dict(a_tau=1., b_tau=1. / d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    kf = kfunc('iso', 1e-8)
+    prng = np.random.RandomState()
+    det = ref_est.LogMarginalLikelihoodLaplaceEstimator(X, y, kf)
+    imp = ref_est.LogMarginalLikelihoodApproxPosteriorISEstimator(
+        X, y, kf, ref_lpa.laplace_approximation)
+    calls = []
+
+    def lp(theta):
+        return (ref_utils.log_gamma_log_pdf(theta[0], prior['a_sigma'], prior['b_sigma']) +
+                ref_utils.log_gamma_log_pdf(theta[1], prior['a_tau'], prior['b_tau']))
+
+    def log_f_adapt(theta):
+        v = det(theta)
+        calls.append(v)
+        return v + lp(theta)
+
+    def log_f_main(theta):
+        v = imp(prng.normal(size=(y.shape[0], n_imp)), theta)[0]
+        calls.append(v)
+        return v + lp(theta)
+
+    def prop_sampler(theta, s):
+        return np.r_[theta[0] + s[0] * prng.normal(), theta[1] + s[1] * prng.normal()]
+
+    def log_prop_density(tp, tc, s):
+        return -0.5 * (((tp[0] - tc[0]) / s[0]) ** 2 + ((tp[1] - tc[1]) / s[1]) ** 2)
+
+    init_scales = np.array([0.5, 0.5])
+    sampler = ref_smp.PMMHSampler(log_f_adapt, log_prop_density, prop_sampler, init_scales, prng)
+    prng.seed(4321)
+    theta_init = np.array([np.log(prng.gamma(prior['a_sigma'], 1. / prior['b_sigma'])),
+                           np.log(prng.gamma(prior['a_tau'], 1. / prior['b_tau']))])
+    ath, aps, aar = sampler.adaptive_run(theta_init, 10, 3, 0.15, 0.30,
+                                         ref_utils.adapt_factor_func, False)
+    n_adapt_calls = len(calls)
+    sampler.log_f_estimator = log_f_main
+    imp.reset_cubic_op_count()
+    thetas, n_reject = sampler.get_samples(ath[-1], 30)
+    np.savez_compressed(os.path.join(HERE, 'pmmh_chain.npz'), X=X, y=y, theta_init=theta_init,
+                        adapt_thetas=ath, adapt_scales=aps, adapt_rates=aar, thetas=thetas,
+                        n_reject=n_reject, n_cubic_ops=imp.n_cubic_ops, calls=np.array(calls),
+                        n_adapt_calls=n_adapt_calls, seed=4321, det_ops=det.n_cubic_ops)
+
+
 def utils_fixture():
     x = np.linspace(-3, 3, 13)
     out = dict(x=x, lgl=ref_utils.log_gamma_log_pdf(x, 1.1, 0.1),
@@ -354,5 +433,6 @@ if __name__ == '__main__':
     sampler_fixture()
     gp_chain_fixture()
     utils_fixture()
+    pmmh_chain_fixture()
     for f in sorted(glob.glob(os.path.join(HERE, '*.npz'))):
         print(os.path.basename(f), os.path.getsize(f))

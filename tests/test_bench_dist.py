@@ -32,3 +32,39 @@ def test_dist_bookkeeping_gloo_world2(tmp_path):
     el, tot, world = float(line[1]), float(line[2]), int(line[3])
     assert world == 2 and tot == 30.0
     assert el >= 0.19  # max over ranks: rank 1 sleeps 2 x 0.1 s
+
+
+def test_rank_streams_disjoint_gloo_world2(tmp_path):
+    """Each rank of `bench.py --gpus 2` drives device LOCAL_RANK with its own sampler seed
+    (bench.chain_seed): the ranks' device indices differ and their 64 chains' Philox keys and
+    host RandomState streams are disjoint (gathered over gloo)."""
+    script = tmp_path / 's.py'
+    script.write_text(textwrap.dedent('''
+        import os, sys
+        sys.path[:0] = [{repo!r}, os.path.join({repo!r}, 'auxiliary-pm-mcmc_amd')]
+        import numpy as np, torch, torch.distributed as tdist
+        import bench
+        from auxpm.batched import chain_streams
+        d = bench.Dist()
+        prngs, keys = chain_streams(bench.chain_seed(20151009, d.rank), 64)
+        first = np.array([r.randint(2 ** 31) for r in prngs], dtype=np.int64)
+        mine = torch.tensor(np.r_[d.local_rank, keys.view(np.int64), first])
+        allv = [torch.zeros_like(mine) for _ in range(d.world)]
+        tdist.all_gather(allv, mine)
+        if d.rank == 0:
+            a, b = allv[0].numpy(), allv[1].numpy()
+            print('RESULT', a[0], b[0], len(set(a[1:65]) & set(b[1:65])),
+                  len(set(a[1:65])), len(set(a[65:]) & set(b[65:])), d.backend)
+        d.close()
+    ''').format(repo=REPO))
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    out = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+                          '--nproc-per-node=2', '--master-addr', '127.0.0.1', '--master-port',
+                          '29534', str(script)], capture_output=True, text=True, env=env,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = [l for l in out.stdout.splitlines() if l.startswith('RESULT')][0].split()
+    assert (r[1], r[2]) == ('0', '1')       # one GPU per rank
+    assert r[3] == '0' and r[4] == '64'     # 64 distinct Philox keys per rank, none shared
+    assert r[5] == '0'                      # host streams start differently on every chain
+    assert r[6] == 'gloo'                   # bookkeeping never creates an RCCL communicator

@@ -1,0 +1,240 @@
+"""Parity at the BASELINE.json configurations themselves (not only at small N):
+
+* configs[2] — N=4096 D=32 ARD-SE, N_imp=256: one batched theta-call of 4 chains (the bench's
+  theta*, a long length-scale, sigma = e^18.5 next to the fp16x3 guard, a prior-like draw) and a
+  cached u-call, against the oracle's CPU restatement of estimators.py:152-241 on the same
+  (theta, u). This is the size the bench runs, with its multi-panel fp16x3 Newton updates, the
+  4-workgroup TRSV, the concurrent chol(K) and the single-launch SYRK.
+* configs[4] — N=16384 D=64 N_imp=1024: the default path against the all-fp32-operand
+  (APM_H3=0) and all-fp64 Newton (APM_MIXED=0) paths on the same inputs (the oracle would take
+  ~10 CPU-minutes here), plus the oracle itself at N=8192 (tools/stress.py's check, as a test).
+* configs[0] — PM-MH, iso kernel, N=768 D=8, N_imp=1, Laplace-estimator adaptive phase then the
+  IS main phase (Pseudo-Marginal MH.ipynb cells 12-14): the reference's own chain
+  (tests/golden/pmmh_chain.npz) replayed with the GPU estimators and the API-compatible
+  PMMHSampler, call by call.
+
+Tolerance for estimator values: |d log f| <= 1e-3 + 2e-7 |log f| (the fp32 L.U
+and epilogue; measured 1e-4 .. 2e-4 at N=4096..8192). n_cubic_ops must be equal and f_post
+within 1e-9 relative (fp64 Newton modes).
+"""
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import apm_oracle as orc
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_ABS, TOL_REL = 1e-3, 2e-7
+
+
+def _tol(r):
+    return TOL_ABS + TOL_REL * abs(r)
+
+
+@pytest.fixture(scope='module')
+def nat(gpu_available):
+    from gpdemo import _native
+    _native.load_library()
+    return _native
+
+
+class _Heartbeat(object):
+    """gpurun treats 3 silent minutes as a hang: print while the CPU oracle runs."""
+
+    def __init__(self, what):
+        self.what = what
+
+    def __enter__(self):
+        self.done = threading.Event()
+        t0 = time.perf_counter()
+
+        def beat():
+            while not self.done.wait(30.):
+                print('{0}: {1:.0f} s'.format(self.what, time.perf_counter() - t0),
+                      file=sys.stderr, flush=True)
+        threading.Thread(target=beat, daemon=True).start()
+        return self
+
+    def __exit__(self, *a):
+        self.done.set()
+
+
+def config2_thetas(d):
+    base = np.log(np.sqrt(d))
+    rng = np.random.RandomState(2024)
+    return np.stack([np.r_[0.0, np.full(d, base)],                        # bench theta*
+                     np.r_[1.0, np.full(d, base + 2.0)],                  # long length-scale
+                     np.r_[18.5, rng.normal(scale=0.2, size=d) + base - 0.5],  # fp16x3 guard edge
+                     np.r_[0.7, rng.normal(scale=0.5, size=d) + base]])   # prior-like
+
+
+def test_config2_full_size_vs_oracle(nat):
+    from gpdemo.utils import synthetic_gp_data
+    n, d, s = 4096, 32, 256
+    X, y = synthetic_gp_data(n, d, 20151009)
+    th = config2_thetas(d)
+    B = th.shape[0]
+    rng = np.random.RandomState(5)
+    U1, U2 = rng.normal(size=(n, s)), rng.normal(size=(n, s))
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=B, n_slots=B, n_ubufs=2)
+    ctx.u_upload(0, U1)
+    ctx.u_upload(1, U2)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, th, [0] * B, list(range(B)))
+    out2, st2 = ctx.u_eval(list(range(B)), [1] * B)
+    fpost = [ctx.slot_read(b)[1] for b in range(B)]
+    ctx.close()
+    assert (st == 0).all() and (st2 == 0).all(), (st, st2)
+    kf = orc.make_kernel_func('ard', 1e-8)
+    K = np.empty((n, n))
+    report = []
+    with _Heartbeat('configs[2] oracle'):
+        for b in range(B):
+            r1, rc, cubic = orc.is_estimate(X, y, kf, U1, th[b], K_work=K)
+            r2, _, _ = orc.is_estimate(X, y, kf, U2, None, rc)
+            report.append((b, out[b] - r1, out2[b] - r2))
+            assert nops[b] == cubic, (b, nops[b], cubic)
+            assert abs(out[b] - r1) <= _tol(r1), (b, out[b], r1)
+            assert abs(out2[b] - r2) <= _tol(r2), (b, out2[b], r2)
+            np.testing.assert_allclose(fpost[b], rc[2], rtol=1e-9,
+                                       atol=1e-9 * np.abs(rc[2]).max())
+    print('configs[2] d(theta-call), d(u-call):', report)
+
+
+def _stress_data(n, d, seed):
+    """tools/stress.py's data (synthetic_gp_data's recipe, distances from one BLAS product)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    'tools'))
+    from stress import stress_data
+    return stress_data(n, d, seed)
+
+
+def _run(nat, X, y, th, s, U, monkeypatch, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    B = th.shape[0]
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=B, n_slots=B, n_ubufs=1)
+    for k in env:
+        monkeypatch.delenv(k)
+    ctx.u_upload(0, U)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, th, [0] * B, list(range(B)))
+    out2, st2 = ctx.u_eval(list(range(B)), [0] * B)
+    f = [ctx.slot_read(b)[1] for b in range(B)]
+    ctx.close()
+    return out, st, nops, out2, f
+
+
+def test_config4_full_size_paths_agree(nat, monkeypatch):
+    n, d, s = 16384, 64, 1024
+    X, y = _stress_data(n, d, 20151009)
+    base = np.log(np.sqrt(d))
+    th = np.stack([np.r_[0.0, np.full(d, base)],
+                   np.r_[2.0, np.random.RandomState(3).normal(scale=0.2, size=d) + base + 0.5]])
+    U = np.random.RandomState(4).normal(size=(n, s))
+    ref = _run(nat, X, y, th, s, U, monkeypatch)
+    assert (ref[1] == 0).all() and np.isfinite(ref[0]).all() and np.isfinite(ref[3]).all()
+    for env in (dict(APM_H3=0), dict(APM_MIXED=0)):
+        o, st, nops, o2, f = _run(nat, X, y, th, s, U, monkeypatch, **env)
+        assert (st == 0).all(), env
+        np.testing.assert_array_equal(nops, ref[2])
+        for b in range(th.shape[0]):
+            assert abs(o[b] - ref[0][b]) <= 1e-5 * max(1., abs(ref[0][b])), (env, b)
+            assert abs(o2[b] - ref[3][b]) <= 1e-5 * max(1., abs(ref[3][b])), (env, b)
+            # the Newton modes of the three paths agree to the refinement's acceptance level
+            # (measured 7e-9 of max|f| at N=16384; 1e-9 at N <= 8192)
+            np.testing.assert_allclose(f[b], ref[4][b], rtol=1e-9,
+                                       atol=2e-8 * np.abs(ref[4][b]).max())
+
+
+def test_config4_scale_n8192_vs_oracle(nat):
+    """The oracle check of tools/stress.py (profiles/r01_stress8k_oracle_check.json) as a test:
+    N=8192, D=64, N_imp=1024, one chain (the oracle's theta-call takes ~1 CPU-minute)."""
+    n, d, s = 8192, 64, 1024
+    X, y = _stress_data(n, d, 20151009)
+    th = np.r_[0.0, np.full(d, np.log(np.sqrt(d)))] + \
+        np.random.RandomState(20151010).normal(scale=0.1, size=d + 1)
+    rng = np.random.RandomState(6)
+    U1, U2 = rng.normal(size=(n, s)), rng.normal(size=(n, s))
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=1, n_slots=1, n_ubufs=2)
+    ctx.u_upload(0, U1)
+    ctx.u_upload(1, U2)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, th[None], [0], [0])
+    out2, _ = ctx.u_eval([0], [1])
+    L, f, _, _ = ctx.slot_read(0)
+    ctx.close()
+    assert st[0] == 0
+    with _Heartbeat('N=8192 oracle'):
+        r1, rc, cubic = orc.is_estimate(X, y, orc.make_kernel_func('ard', 1e-8), U1, th)
+        r2, _, _ = orc.is_estimate(X, y, None, U2, None, rc)
+    print('N=8192 d(theta-call) {0:.3e} d(u-call) {1:.3e}'.format(out[0] - r1, out2[0] - r2))
+    assert nops[0] == cubic
+    assert abs(out[0] - r1) <= _tol(r1), (out[0], r1)
+    assert abs(out2[0] - r2) <= _tol(r2), (out2[0], r2)
+    np.testing.assert_allclose(f, rc[2], rtol=1e-9, atol=1e-9 * np.abs(rc[2]).max())
+    assert np.abs(L - rc[1]).max() <= 1e-6 * np.abs(rc[1]).max()
+
+
+def test_config0_pmmh_chain_matches_reference(nat):
+    import auxpm.samplers as smp
+    import gpdemo.estimators as est
+    import gpdemo.kernels as krn
+    import gpdemo.latent_posterior_approximations as lpa
+    import gpdemo.utils as utils
+    g = golden('pmmh_chain')
+    X, y = g['X'], g['y']
+    d = X.shape[1]
+    prior = dict(a_tau=1., b_tau=1. / d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    kf = krn.make_kernel_func('iso', 1e-8)
+    prng = np.random.RandomState()
+    det = est.LogMarginalLikelihoodLaplaceEstimator(X, y, kf)
+    imp = est.LogMarginalLikelihoodApproxPosteriorISEstimator(X, y, kf, lpa.laplace_approximation)
+    calls = []
+
+    def lp(theta):
+        return (utils.log_gamma_log_pdf(theta[0], prior['a_sigma'], prior['b_sigma']) +
+                utils.log_gamma_log_pdf(theta[1], prior['a_tau'], prior['b_tau']))
+
+    def log_f_adapt(theta):
+        v = det(theta)
+        calls.append(v)
+        return v + lp(theta)
+
+    def log_f_main(theta):
+        v = imp(prng.normal(size=(y.shape[0], 1)), theta)[0]
+        calls.append(v)
+        return v + lp(theta)
+
+    def prop_sampler(theta, sc):
+        return np.r_[theta[0] + sc[0] * prng.normal(), theta[1] + sc[1] * prng.normal()]
+
+    def log_prop_density(tp, tc, sc):
+        return -0.5 * (((tp[0] - tc[0]) / sc[0]) ** 2 + ((tp[1] - tc[1]) / sc[1]) ** 2)
+
+    sampler = smp.PMMHSampler(log_f_adapt, log_prop_density, prop_sampler, np.array([0.5, 0.5]),
+                              prng)
+    prng.seed(int(g['seed']))
+    theta_init = np.array([np.log(prng.gamma(prior['a_sigma'], 1. / prior['b_sigma'])),
+                           np.log(prng.gamma(prior['a_tau'], 1. / prior['b_tau']))])
+    np.testing.assert_array_equal(theta_init, g['theta_init'])
+    ath, aps, aar = sampler.adaptive_run(theta_init, 10, 3, 0.15, 0.30, utils.adapt_factor_func,
+                                         False)
+    na = int(g['n_adapt_calls'])
+    assert len(calls) == na
+    # Laplace phase: fp64 on the device, deterministic
+    np.testing.assert_allclose(calls, g['calls'][:na], rtol=1e-9, atol=1e-9)
+    np.testing.assert_array_equal(ath, g['adapt_thetas'])
+    np.testing.assert_array_equal(aps, g['adapt_scales'])
+    np.testing.assert_array_equal(aar, g['adapt_rates'])
+    sampler.log_f_estimator = log_f_main
+    imp.reset_cubic_op_count()
+    thetas, n_reject = sampler.get_samples(ath[-1], g['thetas'].shape[0])
+    dv = np.abs(np.array(calls[na:]) - g['calls'][na:])
+    assert (dv <= TOL_ABS + TOL_REL * np.abs(g['calls'][na:])).all(), dv.max()
+    np.testing.assert_array_equal(thetas, g['thetas'])
+    assert n_reject == int(g['n_reject'])
+    assert imp.n_cubic_ops == int(g['n_cubic_ops'])

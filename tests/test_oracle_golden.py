@@ -102,3 +102,55 @@ def test_utils_match_reference():
     np.testing.assert_allclose(orc.log_gamma_log_pdf(u['x'], 1.1, 0.1), u['lgl'], rtol=1e-14)
     Xn, mn, sd = orc.normalise_inputs(u['Xraw'])
     np.testing.assert_allclose(Xn, u['Xn'], rtol=1e-14)
+
+
+def test_pushthrough_factor_equals_reference_chol_c():
+    """The device's route to C_chol (chol(K), M = I + L_K^T W L_K, UL Cholesky; DESIGN.md §3.1
+    step 3), restated in fp64 by the oracle, reproduces the reference's chol(C), g, log|B| and
+    estimates on the reference's own outputs."""
+    for ci, c in _cases():
+        pt = orc.theta_state_pushthrough(c['K'], c['y'])
+        rf = orc.theta_state_reformulated(c['K'], c['y'])
+        scale = np.abs(c['C_chol']).max()
+        np.testing.assert_allclose(pt['C_chol'], c['C_chol'], rtol=0, atol=1e-8 * scale)
+        assert abs(pt['logdet_B'] - rf['logdet_B']) < 1e-8 * max(1., abs(rf['logdet_B']))
+        np.testing.assert_allclose(pt['g'], rf['g'], rtol=1e-6, atol=1e-8 * np.abs(rf['g']).max())
+        for ns, key in ((c['ns1'], 'is_logf1'), (c['ns2'], 'is_logf2')):
+            v = orc.is_estimate_reformulated(c['y'], pt, ns)
+            assert abs(v - float(c[key])) < 1e-7 * max(1., abs(float(c[key]))), (ci, key)
+
+
+def test_extreme_theta_errors_match_reference():
+    """Reference behaviour at extreme theta (tests/golden/errors.npz): chol(K) failing raises
+    LinAlgError (estimators.py:206), chol(C) failing raises InvalidCovarianceMatrixError
+    (estimators.py:208-215); the oracle restatement raises the same, with the same message
+    prefix. The push-through route the device takes does not form C and returns a finite
+    state at the InvalidCovarianceMatrixError thetas (the documented deviation)."""
+    e = golden('errors')
+    X, y, ns = e['extreme_X'], e['extreme_y'], e['extreme_ns']
+    kf = orc.make_kernel_func('iso', 1e-8)
+    with pytest.raises(np.linalg.LinAlgError):
+        orc.is_estimate(X, y, kf, ns, e['cholk_theta'])
+    assert str(e['cholk_raised']) == 'LinAlgError'
+    for name in ('icm_a', 'icm_b'):
+        assert str(e[name + '_raised']) == 'InvalidCovarianceMatrixError'
+        with pytest.raises(orc.InvalidCovarianceMatrixError) as ei:
+            orc.is_estimate(X, y, kf, ns, e[name + '_theta'])
+        assert str(ei.value).startswith('Posterior covariance matrix not PSD: sum of negative '
+                                        'eigenvalues -')
+        K = np.empty((X.shape[0],) * 2)
+        kf(K, X, e[name + '_theta'])
+        st = orc.theta_state_pushthrough(K, y)
+        assert np.isfinite(orc.is_estimate_reformulated(y, st, ns))
+
+
+def test_pmmh_chain_fixture_consistent():
+    """configs[0] golden chain (make_golden.py::pmmh_chain_fixture): its recorded estimator
+    calls re-evaluate with the oracle (Laplace phase exactly; IS phase with the same u draws
+    replayed from the seeded prng is checked on the GPU in test_gpu_configs)."""
+    g = golden('pmmh_chain')
+    X, y = g['X'], g['y']
+    kf = orc.make_kernel_func('iso', 1e-8)
+    lml, _ = orc.laplace_estimate(X, y, kf, g['theta_init'])
+    assert abs(lml - float(g['calls'][0])) < 1e-8 * max(1., abs(lml))
+    assert g['thetas'].shape == (30, 2) and int(g['n_adapt_calls']) == 30
