@@ -202,7 +202,21 @@ def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, min_theta_cal
     cores_visible = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') \
         else os.cpu_count()
     cal_files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_cpu_calibration.json')))
-    cal = json.load(open(cal_files[-1])) if cal_files else None
+    cal = None
+    if cal_files:  # port/reference ratio measured in the build container (both on its cores)
+        c = json.load(open(cal_files[-1]))
+        c2 = c['configs2']
+        per_tr = lambda k: (calls_theta * c2[k]['theta_call_s'] +  # noqa: E731
+                            calls_u * c2[k]['u_call_s'])
+        cal = {'source': os.path.relpath(cal_files[-1], REPO), 'host': c['host'],
+               'blas_threads': c['blas_threads'],
+               'ratio_port_over_reference_per_transition': per_tr('port') / per_tr('reference'),
+               'ratio_theta_call': c2['ratio_port_over_reference_theta_call'],
+               'ratio_u_call': c2['ratio_port_over_reference_u_call'],
+               'reference_theta_call_s': c2['reference']['theta_call_s'],
+               'reference_u_call_s': c2['reference']['u_call_s'],
+               'configs0_ratio': c['configs0']['ratio_port_over_reference'],
+               'configs0_reference_iters_per_s': c['configs0']['reference']['iters_per_s']}
     return {
         'value': 1.0 / per_transition, 'unit': 'transitions/s (1 chain)',
         'cores': blas_threads if blas_threads else cores_visible, 'kind': 'port',
