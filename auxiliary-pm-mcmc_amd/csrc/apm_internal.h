@@ -123,9 +123,10 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 // ---- gram.hip -------------------------------------------------------------------------------
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
 // kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
+// both: write both triangles (else K's lower tiles only)
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s);
+                 hipStream_t s, bool both);
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)
@@ -176,9 +177,11 @@ void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t 
                     Live live, int nchains, hipStream_t s);
 void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Live live,
                     int nchains, hipStream_t s);
-// dst (from column dcol0) <- Y2 = J (W^1/2 L)^T J, and L <- L J in place, in one pass
+// dst (from column dcol0) <- Y2 = J (W^1/2 L)^T J, and L <- L J in place, in one pass. Upper
+// tiles of Y2 are zeroed: all of them (zero_all), or only the first super-diagonal, the only
+// ones the single-launch SYRK (k_chol_update_t128, plus == 2) reads
 void launch_form_y2_rev(MatB L, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride,
-                        int np, Live live, int nchains, hipStream_t s);
+                        int np, Live live, int nchains, hipStream_t s, bool zero_all);
 void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s);
 // out = L^T x (L lower), or with rev g = J L^T J h; tile-parallel through nb*nb*64 partials per chain
 void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,

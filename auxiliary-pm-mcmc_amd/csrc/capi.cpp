@@ -70,6 +70,9 @@ struct apm_ctx {
     UPool Up{};
     std::vector<void*> allocs;
     bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix
+    // K's upper triangle holds valid data (host-uploaded K, or the Gram wrote both triangles);
+    // otherwise every K x product uses the symmetric lower-tile kernel (launch_symv)
+    bool k_full = false;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> evpool;
@@ -543,9 +546,12 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         if (mixed) {  // K b and the fp32 B (+ its right-hand side) in one pass over K's lower half
             launch_symv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->sympart, c->sstride,
                         c->np, b32_of(c), c->v.Ws, c->v.vstride, lv, count, c->stream);
-        } else {
+        } else if (c->k_full) {
             launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
                         c->stream);
+        } else {
+            launch_symv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->sympart, c->sstride,
+                        c->np, MatF{}, nullptr, 0, lv, count, c->stream);
         }
         check_launch();
         if (mixed) {
@@ -562,7 +568,7 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         }
         launch_newton_update(c->v, c->np, lv, count, c->stream);
         check_launch();
-        if (mixed)
+        if (mixed || !c->k_full)
             launch_symv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->sympart,
                         c->sstride, c->np, MatF{}, nullptr, 0, lv, count, c->stream);
         else
@@ -715,12 +721,13 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
         launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
         check_launch();
     }
-    launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s);  // Y2 = J Z^T J, Y = L_K J
-    check_launch();
     // J M J = I + Y2 Y2^T: on the 128x128 super-tile path one launch writes it without reading TL
     // (tile column j takes Y2's column blocks k <= j); otherwise TL starts as I and receives
     // panel-wide updates (Y2 lower: j >= K suffices)
-    if ((c->t128 & 2) && nb >= 2) {
+    const bool syrk1 = (c->t128 & 2) && nb >= 2;
+    launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s, !syrk1);  // Y2, Y = L_K J
+    check_launch();
+    if (syrk1) {
         tracked_update(c, TL, nb, nb, 0, nb, 0, nb, Gap{0, 0}, 2, count);
     } else {
         launch_identity_lower(TL, np, lv, count, s);
@@ -744,10 +751,13 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
     if (gram) {
-        ProfScope ps(c, APM_PROF_GRAM,
-                     8.0 * ((double)c->n * c->d + (double)c->n * c->n) * count + 8.0 * c->P);
+        // the augmented posterior route (APM_POSTCOV=aug) reads K's upper tiles; every other
+        // consumer reads the lower ones: the Gram then writes N(N+1)/2 entries
+        c->k_full = c->postcov_aug;
+        const double nk = c->k_full ? (double)c->n * c->n : 0.5 * (double)c->n * (c->n + 1);
+        ProfScope ps(c, APM_PROF_GRAM, 8.0 * ((double)c->n * c->d + nk) * count + 8.0 * c->P);
         launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
-                    count, c->stream);
+                    count, c->stream, c->k_full);
         check_launch();
     }
     std::vector<int> st_h(count, 0), it_h(count, 0);
@@ -1146,6 +1156,7 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
                     (i < c->n && j < c->n) ? K[(int64_t)i * ldk + j] : (i == j ? 1.0 : 0.0);
         HIPC(hipMemcpyAsync(c->K.base, Kp.data(), sizeof(double) * Kp.size(),
                             hipMemcpyHostToDevice, c->stream));
+        c->k_full = true;
         double kmax = 0.0;
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
         pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
@@ -1241,7 +1252,7 @@ int apm_gram(int device, int kind, const double* X, int64_t n, int64_t d, int64_
         HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
         launch_gram(c->K, c->X, d, (int)n, (int)d, c->theta, P, kind, eps, c->np, live_of(c), 1,
-                    c->stream);
+                    c->stream, true);
         check_launch();
         HIPC(hipMemcpy2DAsync(K, sizeof(double) * ldk, c->K.base, sizeof(double) * c->np,
                               sizeof(double) * n, n, hipMemcpyDeviceToHost, c->stream));
@@ -1286,6 +1297,7 @@ int apm_laplace(int device, const double* K, int64_t n, int64_t ldk, const doubl
                     (i < n && j < n) ? K[(int64_t)i * ldk + j] : (i == j ? 1.0 : 0.0);
         HIPC(hipMemcpyAsync(c->K.base, Kp.data(), sizeof(double) * Kp.size(), hipMemcpyHostToDevice,
                             c->stream));
+        c->k_full = true;
         HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
         HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int), c->stream));

@@ -2,7 +2,9 @@
 //
 //   isotropic_squared_exponential_kernel  kernels.pyx:12-49   K_ij = s exp(-|x_i-x_j|^2 / (2 tau^2))
 //   diagonal_squared_exponential_kernel   kernels.pyx:52-90   K_ij = s exp(-1/2 sum_k ((x_ik-x_jk)/tau_k)^2)
-//   K_ii = s + eps; both triangles written (the reference fills K[i,j] and K[j,i]).
+//   K_ii = s + eps. both != 0: both triangles written (the reference fills K[i,j] and K[j,i];
+//   the stand-alone apm_gram); both == 0: lower tiles only (the theta-call: every consumer on the
+//   device path reads K's lower tiles, so the upper half is never written - half the bytes).
 // One workgroup per lower tile (i >= j) of 64x64; X row blocks are staged through LDS in chunks of
 // 32 features, multiplied by 1/tau_k on the way in (2 fp64 VALU ops per pair and feature); the tile
 // and its transpose are written with 32-byte contiguous runs per thread (coalesced 512-byte rows).
@@ -16,7 +18,8 @@
 
 __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__ X, int64_t ldx,
                                               int n, int d, const double* __restrict__ theta,
-                                              int64_t tstride, int kind, double eps, Live live) {
+                                              int64_t tstride, int kind, double eps, Live live,
+                                              int both) {
     const int b = blockIdx.y;
     if (live.active[b] == 0 || live.status[b] != 0) return;
     // lower-triangular tile index -> (ti, tj), ti >= tj
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__
         *reinterpret_cast<d2_t*>(dst + 2 * tc) = d2_t{v[p][0], v[p][1]};
         *reinterpret_cast<d2_t*>(dst + 32 + 2 * tc) = d2_t{v[p][2], v[p][3]};
     }
-    if (ti != tj) {  // transposed tile (tj, ti)
+    if (both && ti != tj) {  // transposed tile (tj, ti)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             double* dst = Kb + (int64_t)(tj * 64 + RO(tc, q)) * K.ld + ti * 64;
@@ -104,8 +107,8 @@ __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__
 
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s) {
+                 hipStream_t s, bool both) {
     const int nb = np / 64;
     hipLaunchKernelGGL(k_gram, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx, n,
-                       d, theta, tstride, kind, eps, live);
+                       d, theta, tstride, kind, eps, live, (int)both);
 }

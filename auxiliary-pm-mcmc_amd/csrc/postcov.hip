@@ -71,7 +71,7 @@ __device__ __forceinline__ void load_lower_tile(const double* Lr, int64_t ld, in
 // Y2 tile of source tile (sr, sc) (as k_form_y2); T must be free on entry
 __device__ __forceinline__ void y2_tile(double (*T)[65], const d2_t v[8], int sr, int sc,
                                         double* dbase, int64_t ld, int64_t dcol0,
-                                        const double* w, int nb) {
+                                        const double* w, int nb, int zero_all) {
     const int ta = nb - 1 - sc, tk = nb - 1 - sr, np = nb * 64;
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
@@ -81,7 +81,8 @@ __device__ __forceinline__ void y2_tile(double (*T)[65], const d2_t v[8], int sr
     }
     __syncthreads();
     double* D = dbase + (int64_t)(ta * 64) * ld + dcol0 + tk * 64;
-    if (tk > ta) {
+    if (tk > ta) {  // upper tile of Y2: zero where the SYRK reads it
+        if (!zero_all && tk != ta + 1) return;
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const int e = threadIdx.x + 256 * h;
@@ -101,7 +102,8 @@ __device__ __forceinline__ void y2_tile(double (*T)[65], const d2_t v[8], int sr
 
 __global__ __launch_bounds__(256) void k_form_y2_rev(MatB L, MatB dst, int64_t dcol0,
                                                      const double* __restrict__ Ws,
-                                                     int64_t vstride, int nb, Live live) {
+                                                     int64_t vstride, int nb, Live live,
+                                                     int zero_all) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
     const int half = (nb + 1) / 2;
@@ -113,10 +115,10 @@ __global__ __launch_bounds__(256) void k_form_y2_rev(MatB L, MatB dst, int64_t d
     d2_t p[8], q[8];
     load_lower_tile(Lr, L.ld, sr, c1, p);
     if (c2 != c1) load_lower_tile(Lr, L.ld, sr, c2, q);
-    y2_tile(T, p, sr, c1, dbase, dst.ld, dcol0, w, nb);
+    y2_tile(T, p, sr, c1, dbase, dst.ld, dcol0, w, nb, zero_all);
     __syncthreads();
     if (c2 != c1) {
-        y2_tile(T, q, sr, c2, dbase, dst.ld, dcol0, w, nb);
+        y2_tile(T, q, sr, c2, dbase, dst.ld, dcol0, w, nb, zero_all);
     } else {
 #pragma unroll
         for (int h = 0; h < 8; ++h) q[h] = p[h];
@@ -131,10 +133,10 @@ __global__ __launch_bounds__(256) void k_form_y2_rev(MatB L, MatB dst, int64_t d
 }
 
 void launch_form_y2_rev(MatB L, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride,
-                        int np, Live live, int nchains, hipStream_t s) {
+                        int np, Live live, int nchains, hipStream_t s, bool zero_all) {
     const int nb = np / 64;
     hipLaunchKernelGGL(k_form_y2_rev, dim3(nb * ((nb + 1) / 2), nchains), dim3(256), 0, s, L, dst,
-                       dcol0, Ws, vstride, nb, live);
+                       dcol0, Ws, vstride, nb, live, (int)zero_all);
 }
 
 // lower tiles of M <- I

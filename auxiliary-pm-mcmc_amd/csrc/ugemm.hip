@@ -110,12 +110,24 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
                                                UPool P, const int64_t* __restrict__ ubufs,
                                                const double* __restrict__ y, int n, int np,
                                                double* __restrict__ partial, int64_t pstride,
-                                               const int* __restrict__ status) {
-    const int b = blockIdx.z;
-    if (status[b] != 0) return;
+                                               const int* __restrict__ status, int nsb,
+                                               int nchains) {
+    // XCD-aware order (as k_chol_update's xcd_remap): dispatch slot s runs on XCD s % 8, and
+    // consecutive work items land on the same XCD. Items run chain-major, then row block
+    // (heaviest, i.e. longest K range, first; consecutive row blocks read nearly the same rows
+    // of U), then sample block fastest - so the nsb
+    // workgroups that share row block i's slice of L run together on one XCD and read it once
+    // from its L2, and a chain's U stays within one XCD's L2 / the Infinity Cache.
     const int nb = np / 64;
-    const int i = nb - (int)blockIdx.x;  // heaviest row blocks (longest K range) first
-    const int sb = blockIdx.y;
+    const long total = (long)(nb + 1) * nsb * nchains;
+    const long slot_id = blockIdx.x, xcd = slot_id & 7, q = total >> 3, rem = total & 7;
+    const long item = nchains < 8 ? slot_id  // too few chains to fill 8 XCDs evenly: plain order
+                      : (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (slot_id >> 3);
+    const int b = (int)(item / ((long)(nb + 1) * nsb));
+    const int rest = (int)(item % ((long)(nb + 1) * nsb));
+    if (status[b] != 0) return;
+    const int i = nb - rest / nsb;
+    const int sb = rest % nsb;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     __shared__ float Ut[2][64][UP];
@@ -226,9 +238,10 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
 void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
                   const double* y, int n, int np, double* partial, int64_t pstride,
                   const int* status, int nchains, hipStream_t s) {
-    const int nb = np / 64;
-    hipLaunchKernelGGL(k_ugemm, dim3(nb + 1, P.sp / 64, nchains), dim3(256), 0, s, S, slots, P,
-                       ubufs, y, n, np, partial, pstride, status);
+    const int nb = np / 64, nsb = P.sp / 64;
+    const long total = (long)(nb + 1) * nsb * nchains;
+    hipLaunchKernelGGL(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
+                       np, partial, pstride, status, nsb, nchains);
 }
 
 // logsumexp_s(lw_s) - log S per chain

@@ -8,7 +8,14 @@ per-dispatch HBM traffic, corrected as MI355X_MICROARCH.md §HBM prescribes: FET
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-byte-per-lane reads
 (x2 here); WRITE_SIZE is exact for 16-byte-per-lane stores (8-byte stores are uncalibrated).
 
-usage: prof_window.py trace.csv [--fetch fetch.csv --write write.csv] [--out out.json]
+Given the counter_collection CSV of a `--pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE` pass it
+also writes per-kernel MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES sums the busy cycles of every
+MFMA over all 1024 SIMDs, GRBM_GUI_ACTIVE sums the dispatch's active cycles over the 8 XCDs
+(MI355X_MICROARCH.md: DVFS note), so util = MFMA_BUSY / (1024 x GRBM_GUI_ACTIVE / 8). Counter
+passes serialise dispatches (no overlap with the concurrent chol(K) stream).
+
+usage: prof_window.py trace.csv [--fetch fetch.csv --write write.csv] [--mfma mfma.csv]
+                      [--out out.json]
 """
 import argparse
 import collections
@@ -39,6 +46,7 @@ def main():
     ap.add_argument('trace')
     ap.add_argument('--fetch')
     ap.add_argument('--write')
+    ap.add_argument('--mfma')
     ap.add_argument('--out')
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
@@ -76,6 +84,26 @@ def main():
         out['pmc_traffic'] = traffic
         out['pmc_correction'] = ('read = 2 x FETCH_SIZE (KiB, gfx950 half-count of 16 B/lane '
                                  'reads), write = WRITE_SIZE (KiB); MI355X_MICROARCH.md HBM')
+    if a.mfma:
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        rows = list(csv.DictReader(open(a.mfma)))
+        win = window(rows, 'Kernel_Name', 'Start_Timestamp', 'End_Timestamp')
+        disp = collections.defaultdict(set)
+        for r in win:
+            k = short(r['Kernel_Name'])
+            per[k][r['Counter_Name']] += float(r['Counter_Value'])
+            disp[k].add(r.get('Dispatch_Id', r['Start_Timestamp']))
+        util = {}
+        for k, d in per.items():
+            busy, act = d.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0), d.get('GRBM_GUI_ACTIVE', 0.0)
+            if act > 0 and busy > 0:
+                util[k] = {'dispatches': len(disp[k]), 'mfma_busy_cycles': busy,
+                           'grbm_gui_active': act, 'mfma_util': busy / (1024.0 * act / 8.0)}
+        out['pmc_mfma'] = dict(sorted(util.items(), key=lambda x: -x[1]['mfma_busy_cycles']))
+        out['pmc_mfma_formula'] = ('SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 '
+                                   'XCDs), summed over the timed window\'s dispatches')
+        for k, v in list(out['pmc_mfma'].items())[:8]:
+            print('mfma {0:28s} {1:6d} util {2:6.1%}'.format(k, v['dispatches'], v['mfma_util']))
     if a.out:
         json.dump(out, open(a.out, 'w'), indent=1)
 
