@@ -1,24 +1,31 @@
 # -*- coding: utf-8 -*-
-"""Many independent APM chains advanced together on one MI355X.
+"""Many independent APM / PM chains advanced together on one MI355X.
 
-``BatchedAPMEllSSPlusRandDirSliceSampler`` runs ``n_chains`` copies of the reference's
-``APMEllSSPlusRandDirSliceSampler`` transition (elliptical slice sampling on the auxiliary
-draws u, random-direction linear slice sampling on theta; reference samplers.py:1007-1089 with
-mcmc_updates.py:311-400, :403-519). Two schedules share the per-chain code:
+Three batched twins of the reference samplers share one device context, the per-chain random
+streams and the masked-failure bookkeeping (``_BatchedChains``):
 
-* ``step()``: lockstep — every chain does one whole transition; each shrink iteration of every
-  still-undecided chain is one batched estimator call (late rounds carry few chains).
-* ``run(...)`` / ``run_async(...)``: asynchronous — each chain is a small state machine and every
-  round issues ONE batched theta-call for all chains whose random-direction slice step needs an
-  evaluation, after first completing (with cheap batched u-calls) the elliptical slice update of
-  every chain that has just finished a transition. Chains never wait for each other, so every
-  theta-call carries the whole batch. Each chain's sequence of estimator calls and host-RNG draws
-  is unchanged, so its trajectory is identical to the lockstep (and, up to the device u, to the
-  reference's sequential) run; tests/test_gpu_batched.py checks async == lockstep bitwise.
+* ``BatchedAPMEllSSPlusRandDirSliceSampler`` — ``APMEllSSPlusRandDirSliceSampler`` (reference
+  samplers.py:1007-1089; elliptical slice sampling on u, random-direction linear slice sampling
+  on theta; mcmc_updates.py:311-400, :403-519; BASELINE configs[2]/[3]). Two schedules:
+  ``step()`` lockstep (each shrink round of every still-undecided chain is one batched call) and
+  ``run(...)`` / ``run_async(...)`` asynchronous (every round issues ONE batched theta-call for
+  all chains whose slice step needs an evaluation, after completing with cheap batched u-calls
+  the elliptical slice update of every chain that has just finished a transition).
+* ``BatchedAPMEllSSPlusMHSampler`` — ``APMEllSSPlusMHSampler`` (samplers.py:421-585;
+  BASELINE configs[1]): E-SS on u (batched u-calls), then one Metropolis(-Hastings) theta step
+  per chain — exactly one theta-call per transition, so every theta-call carries the whole batch
+  in lockstep; proposal/current cache slots as samplers.py:563-584 (the proposal's slot becomes
+  current on accept).
+* ``BatchedPMMHSampler`` — ``PMMHSampler`` (samplers.py:159-262; BASELINE configs[0] protocol,
+  Pseudo-Marginal MH.ipynb cells 12-14): one batched theta-call per iteration at the proposals,
+  with the Laplace estimator (adaptive phase) or the IS estimator on fresh u (main phase).
 
 Per chain the control flow, the cache protocol and the host-RNG draw order are those of the
-reference (one ``numpy.random.RandomState`` per chain for the slice heights, angles, offsets and
-directions). The auxiliary draws u and nu live on the device: they are produced by Philox4x32-10
+reference (one ``numpy.random.RandomState`` per chain for slice heights, angles, offsets,
+directions, proposals and accept uniforms). Each chain's streams depend only on (seed, chain
+index) (``chain_streams``), and every device kernel computes each chain independently of the
+others in its batch, so a chain's trajectory does not depend on the batch it runs in
+(tests/test_gpu_batched.py). The auxiliary draws u and nu live on the device: Philox4x32-10
 (one counter stream per chain) and the E-SS proposal u cos(phi) + nu sin(phi) is formed on the
 device, so trajectories are statistically — not bitwise — equivalent to a numpy-u_sampler run
 (DESIGN.md §6). The log target is estimator + log-Gamma prior (E-SS+RD-SS.ipynb:167-173), the
@@ -32,37 +39,36 @@ import numpy as np
 from gpdemo import _native
 from gpdemo.utils import log_prior_ard_batch
 
-__all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler', 'chain_streams']
+__all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler', 'BatchedAPMEllSSPlusMHSampler',
+           'BatchedPMMHSampler', 'chain_streams']
 
-_EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC}
+_EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC, 'laplace': _native.EST_LAPLACE}
 
 
-def chain_streams(seed, n_chains):
-    """Per-chain random streams of a batch: numpy.random.SeedSequence(seed).spawn(n_chains)
-    gives each chain a host RandomState (MT19937; slice heights, angles, directions, MH draws)
+def chain_streams(seed, n_chains, first_chain=0):
+    """Per-chain random streams: chain c gets numpy.random.SeedSequence(seed, spawn_key=(c,)) —
+    the c-th child of SeedSequence(seed).spawn(...), whatever the batch size — which seeds a
+    host RandomState (MT19937; slice heights, angles, directions, proposals, accept uniforms)
     and a 64-bit Philox4x32-10 key for its device draws (u, nu). Different `seed`s (bench.py
     derives one per rank) give statistically independent, non-overlapping streams."""
-    kids = np.random.SeedSequence(seed).spawn(n_chains)
+    kids = [np.random.SeedSequence(seed, spawn_key=(first_chain + c,)) for c in range(n_chains)]
     prngs = [np.random.RandomState(np.random.MT19937(k)) for k in kids]
     dev_seeds = np.array([k.generate_state(2, np.uint64)[0] for k in kids], dtype=np.uint64)
     return prngs, dev_seeds
 
 
-class BatchedAPMEllSSPlusRandDirSliceSampler(object):
-    """Lockstep batch of APM E-SS(u) + RD-SS(theta) chains on one device.
+class _BatchedChains(object):
+    """Device context, per-chain streams and state shared by the batched samplers.
 
-    Parameters mirror the notebook protocol: ``kernel`` 'ard' | 'iso', ``epsilon`` jitter,
-    ``n_imp`` importance samples, slice width ``w`` and ``max_steps_out`` (E-SS+RD-SS.ipynb:64-67),
-    ``prior`` the log-Gamma hyper-parameters (a_sigma, b_sigma, a_tau, b_tau).
-    """
+    Buffers per chain: cache slots ``slot_cur`` / ``slot_prop`` (samplers.py:563-584: the
+    current state's cache and the proposal's), u buffers ``ub_u`` (current u), ``ub_nu`` (E-SS
+    auxiliary draw) and ``ub_prop`` (proposed u)."""
 
-    def __init__(self, X, y, n_chains, n_imp, prior, kernel='ard', epsilon=1e-8, w=1.,
-                 max_steps_out=0, max_slice_iters=1000, seed=0, estimator='is', device=None):
+    def __init__(self, X, y, n_chains, n_imp, prior, kernel='ard', epsilon=1e-8,
+                 max_slice_iters=1000, seed=0, estimator='is', device=None, first_chain=0):
         self.n_chains = int(n_chains)
         self.n_imp = int(n_imp)
         self.prior = dict(prior)
-        self.w = float(w)
-        self.max_steps_out = int(max_steps_out)
         self.max_slice_iters = int(max_slice_iters)
         self.est = _EST[estimator]
         kind = _native.KERNEL_ARD if kernel == 'ard' else _native.KERNEL_ISO
@@ -75,7 +81,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.ub_u = np.arange(C, dtype=np.int64)
         self.ub_nu = np.arange(C, 2 * C, dtype=np.int64)
         self.ub_prop = np.arange(2 * C, 3 * C, dtype=np.int64)
-        self.prngs, self.dev_seeds = chain_streams(seed, C)
+        self.prngs, self.dev_seeds = chain_streams(seed, C, first_chain)
         self.dev_ctr = np.zeros(C, dtype=np.uint64)
         self.theta = np.zeros((C, self.P))
         self.log_f = np.full(C, -np.inf)
@@ -87,18 +93,6 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.n_cubic_ops = np.zeros(C, dtype=np.int64)
         # wall seconds inside the device calls (the rest of a run is host-side sampler logic)
         self.wall = {'theta_call': 0., 'u_call': 0., 'u_draw': 0.}
-        # asynchronous random-direction slice state (one pending theta per chain)
-        self._rd_d = np.zeros((C, self.P))
-        self._rd_logy = np.zeros(C)
-        self._rd_lo = np.zeros(C)
-        self._rd_hi = np.zeros(C)
-        self._rd_x = np.zeros(C)
-        self._rd_mode = np.zeros(C, dtype=np.int64)  # 0: step down, 1: step up, 2: shrink
-        self._rd_s = np.zeros(C, dtype=np.int64)
-        self._rd_down = np.zeros(C)
-        self._rd_up = np.zeros(C)
-        self._rd_it = np.zeros(C, dtype=np.int64)
-        self._rd_pend = np.zeros((C, self.P))
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
@@ -110,10 +104,14 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
         self.wall['u_draw'] += time.perf_counter() - t0
         self.dev_ctr[idx] += 1
 
-    def _theta_eval(self, idx, thetas, slots):
+    def _theta_eval(self, idx, thetas, slots, ubufs=None):
         """Batched theta-call; returns (log target, log prior) of each proposal."""
         t0 = time.perf_counter()
-        out, st, nops = self.ctx.theta_eval(self.est, thetas, self.ub_u[idx], slots)
+        ub = self.ub_u[idx] if ubufs is None else ubufs
+        if self.est == _native.EST_LAPLACE:
+            out, st, nops = self.ctx.theta_eval(self.est, thetas)
+        else:
+            out, st, nops = self.ctx.theta_eval(self.est, thetas, ub, slots)
         self.wall['theta_call'] += time.perf_counter() - t0
         self.n_theta_calls += len(idx)
         self.n_cubic_ops[idx] += nops
@@ -191,6 +189,37 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
                 keep.append(c)
             act = np.array(keep, dtype=np.int64)
             it += 1
+
+
+class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
+    """Batch of APM E-SS(u) + RD-SS(theta) chains on one device.
+
+    Parameters mirror the notebook protocol: ``kernel`` 'ard' | 'iso', ``epsilon`` jitter,
+    ``n_imp`` importance samples, slice width ``w`` and ``max_steps_out`` (E-SS+RD-SS.ipynb:64-67),
+    ``prior`` the log-Gamma hyper-parameters (a_sigma, b_sigma, a_tau, b_tau).
+    """
+
+    def __init__(self, X, y, n_chains, n_imp, prior, kernel='ard', epsilon=1e-8, w=1.,
+                 max_steps_out=0, max_slice_iters=1000, seed=0, estimator='is', device=None,
+                 first_chain=0):
+        super(BatchedAPMEllSSPlusRandDirSliceSampler, self).__init__(
+            X, y, n_chains, n_imp, prior, kernel, epsilon, max_slice_iters, seed, estimator,
+            device, first_chain)
+        self.w = float(w)
+        self.max_steps_out = int(max_steps_out)
+        C = self.n_chains
+        # asynchronous random-direction slice state (one pending theta per chain)
+        self._rd_d = np.zeros((C, self.P))
+        self._rd_logy = np.zeros(C)
+        self._rd_lo = np.zeros(C)
+        self._rd_hi = np.zeros(C)
+        self._rd_x = np.zeros(C)
+        self._rd_mode = np.zeros(C, dtype=np.int64)  # 0: step down, 1: step up, 2: shrink
+        self._rd_s = np.zeros(C, dtype=np.int64)
+        self._rd_down = np.zeros(C)
+        self._rd_up = np.zeros(C)
+        self._rd_it = np.zeros(C, dtype=np.int64)
+        self._rd_pend = np.zeros((C, self.P))
 
     def _rdss_theta(self):
         """Random-direction linear slice update of every live chain's theta
@@ -397,3 +426,166 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(object):
                 thetas[c, 1:1 + k] = np.array(traces[c])
             thetas[c, 1 + k:] = self.theta[c]  # failed chains: frozen at their last state
         return thetas
+
+
+class _BatchedMHMixin(object):
+    """Per-chain Metropolis(-Hastings) decisions of a batch of proposals, in the reference's
+    draw order and expressions (mcmc_updates.py:14-156; the notebooks' componentwise Gaussian
+    random-walk proposal theta + s * N(0, I) and its log density, e.g. Pseudo-Marginal
+    MH.ipynb cell 12). ``prop_scales``: (P,) shared or (n_chains, P) per chain; adapted per
+    chain by ``adaptive_run``."""
+
+    def _init_mh(self, prop_scales, metropolis):
+        self.prop_scales = np.array(np.broadcast_to(np.asarray(prop_scales, dtype=np.float64),
+                                                    (self.n_chains, self.P)))
+        self.metropolis = bool(metropolis)
+        self.n_reject = np.zeros(self.n_chains, dtype=np.int64)
+
+    def _propose(self, live):
+        th = self.theta[live].copy()
+        for q, c in enumerate(live):
+            th[q] = self.theta[c] + self.prop_scales[c] * self.prngs[c].normal(size=self.P)
+        return th
+
+    @staticmethod
+    def _log_prop_density(x_to, x_from, s):
+        return -0.5 * np.sum(((x_to - x_from) / s) ** 2)
+
+    def _decide(self, live, th_p, lf_p, lp_p, on_accept):
+        """accept iff U < exp(log f' - log f) [Metropolis] or the MH ratio (reference
+        metropolis_step / met_hastings_step); returns the rejection mask."""
+        rej = np.zeros(len(live), dtype=bool)
+        for q, c in enumerate(live):
+            if self.metropolis:
+                p_acc = np.exp(lf_p[q] - self.log_f[c])
+            else:
+                s = self.prop_scales[c]
+                log_q_fwd = self._log_prop_density(th_p[q], self.theta[c], s)
+                log_q_bwd = self._log_prop_density(self.theta[c], th_p[q], s)
+                p_acc = np.exp(lf_p[q] + log_q_bwd - self.log_f[c] - log_q_fwd)
+            if self.prngs[c].uniform() < p_acc:
+                self.theta[c] = th_p[q]
+                self.log_f[c] = lf_p[q]
+                self.lp_cur[c] = lp_p[q]
+                on_accept(c)
+            else:
+                rej[q] = True
+                self.n_reject[c] += 1
+        return rej
+
+    def get_samples(self, n_sample, theta_init=None):
+        """(thetas (n_chains, n_sample, P), n_reject (n_chains,)) from the current state (or a
+        fresh start at theta_init), as the reference get_samples (first row = start state);
+        failed chains are frozen at their last state."""
+        if theta_init is not None or not np.isfinite(self.log_f).any():
+            self.initialise(theta_init)
+        thetas = np.empty((self.n_chains, n_sample, self.P))
+        thetas[:, 0] = self.theta
+        self.n_reject[:] = 0
+        for s in range(1, n_sample):
+            thetas[:, s] = self.step()
+        return thetas, self.n_reject.copy()
+
+    def adaptive_run(self, theta_init, batch_size, n_batch, low_acc_thr, upp_acc_thr,
+                     adapt_factor_func):
+        """BaseAdaptiveMHSampler.adaptive_run (samplers.py:14-156) for every chain: each batch
+        restarts get_samples from the previous batch's last state (a fresh estimate there, as
+        the reference's get_samples does) and each chain's scales are divided / multiplied by
+        adapt_factor_func(b, n_batch) when its batch accept rate is below / above the
+        thresholds. Returns (thetas (C, n_batch*batch_size, P), scales (C, n_batch, P),
+        accept_rates (C, n_batch))."""
+        C = self.n_chains
+        thetas = np.empty((C, n_batch * batch_size, self.P))
+        scales = np.empty((C, n_batch, self.P))
+        rates = np.empty((C, n_batch))
+        th0 = np.array(theta_init, dtype=np.float64)
+        for b in range(n_batch):
+            lo, hi = b * batch_size, (b + 1) * batch_size
+            thetas[:, lo:hi], n_reject = self.get_samples(batch_size, th0)
+            rates[:, b] = 1. - (n_reject * 1. / batch_size)
+            th0 = thetas[:, hi - 1].copy()
+            factor = adapt_factor_func(b, n_batch)
+            for c in range(C):
+                if rates[c, b] < low_acc_thr:
+                    self.prop_scales[c] /= factor
+                elif rates[c, b] > upp_acc_thr:
+                    self.prop_scales[c] *= factor
+            scales[:, b] = self.prop_scales
+        return thetas, scales, rates
+
+
+class BatchedAPMEllSSPlusMHSampler(_BatchedMHMixin, _BatchedChains):
+    """Batch of APM E-SS(u) + MH(theta) chains (reference APMEllSSPlusMHSampler,
+    samplers.py:421-585; BASELINE configs[1]). ``metropolis=False`` uses met_hastings_step with
+    the Gaussian proposal density, as the E-SS+MH notebook passes ``log_prop_density``."""
+
+    def __init__(self, X, y, n_chains, n_imp, prior, prop_scales, kernel='ard', epsilon=1e-8,
+                 metropolis=False, max_slice_iters=1000, seed=0, estimator='is', device=None,
+                 first_chain=0):
+        super(BatchedAPMEllSSPlusMHSampler, self).__init__(
+            X, y, n_chains, n_imp, prior, kernel, epsilon, max_slice_iters, seed, estimator,
+            device, first_chain)
+        self._init_mh(prop_scales, metropolis)
+
+    def _mh_theta(self):
+        """One batched theta-call at every live chain's proposal (with its current u) into the
+        proposal slot; on accept the proposal's slot becomes current (samplers.py:563-584)."""
+        live = np.flatnonzero(~self.failed)
+        if live.size == 0:
+            return
+        th_p = self._propose(live)
+        lf_p, lp_p = self._theta_eval(live, th_p, self.slot_prop[live])
+
+        def accept(c):
+            self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
+        self._decide(live, th_p, lf_p, lp_p, accept)
+
+    def step(self):
+        """One transition of every live chain (u by E-SS, then theta by MH); returns thetas."""
+        self._ess_u()
+        self._mh_theta()
+        return self.theta.copy()
+
+
+class BatchedPMMHSampler(_BatchedMHMixin, _BatchedChains):
+    """Batch of pseudo-marginal MH chains (reference PMMHSampler, samplers.py:159-262; the
+    protocol of Pseudo-Marginal MH.ipynb). Every iteration draws each chain's proposal, and with
+    the IS estimator a fresh u on the device, and evaluates all proposals in ONE batched
+    theta-call; the current state's estimate is recycled. ``set_estimator('laplace')`` gives the
+    deterministic Laplace-LML adaptive phase, ``'is'`` the importance-sampling main phase
+    (``sampler.log_f_estimator = log_f_estimator_main`` in the notebook)."""
+
+    def __init__(self, X, y, n_chains, n_imp, prior, prop_scales, kernel='iso', epsilon=1e-8,
+                 metropolis=False, seed=0, estimator='is', device=None, first_chain=0):
+        super(BatchedPMMHSampler, self).__init__(
+            X, y, n_chains, n_imp, prior, kernel, epsilon, 1000, seed, estimator, device,
+            first_chain)
+        self._init_mh(prop_scales, metropolis)
+
+    def set_estimator(self, estimator):
+        self.est = _EST[estimator]
+        self.log_f[:] = -np.inf  # the next get_samples starts with a fresh estimate
+
+    def initialise(self, theta_init=None):
+        """The start state's estimate (PMMHSampler.get_samples: log_f_estimator(theta_init))."""
+        idx = np.arange(self.n_chains)
+        self.theta = self.prior_draw() if theta_init is None else np.array(theta_init, float)
+        if self.est != _native.EST_LAPLACE:
+            self._normals(idx, self.ub_u)
+        self.log_f, self.lp_cur = self._theta_eval(idx, self.theta, self.slot_cur[idx])
+        return self.theta.copy()
+
+    def step(self):
+        live = np.flatnonzero(~self.failed)
+        if live.size == 0:
+            return self.theta.copy()
+        th_p = self._propose(live)
+        if self.est != _native.EST_LAPLACE:
+            self._normals(live, self.ub_prop)  # fresh u for every proposal
+        lf_p, lp_p = self._theta_eval(live, th_p, self.slot_prop[live], self.ub_prop[live])
+
+        def accept(c):
+            self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
+            self.ub_u[c], self.ub_prop[c] = self.ub_prop[c], self.ub_u[c]
+        self._decide(live, th_p, lf_p, lp_p, accept)
+        return self.theta.copy()

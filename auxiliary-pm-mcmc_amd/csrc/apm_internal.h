@@ -68,6 +68,7 @@ void launch_trsv_lt_step(MatB A, int J, int64_t rrow, const double* Dinv, int64_
 void launch_marker(int id, hipStream_t s);
 // test hook: C(64x64) = A(64x64) * B(64x64)^T through the MFMA tile path
 void launch_tile_nt_test(const double* A, const double* B, double* C, hipStream_t s);
+void launch_philox_test(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s);
 
 // ---- chol32.hip: mixed-precision Newton solve (fp32 factor of B + fp64 refinement) -----------
 void launch_chol_diag32(MatF A, int k, float* Dinv, int64_t dstride, double* ldet,

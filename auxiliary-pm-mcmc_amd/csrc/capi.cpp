@@ -1361,6 +1361,25 @@ int apm_selftest_tile(int device, const double* A, const double* B, double* C) {
     return APM_SUCCESS;
 }
 
+int apm_selftest_philox(int device, int64_t n, const uint32_t* in, uint32_t* out) {
+    if (!in || !out || n <= 0 || n > (1 << 24))
+        return fail(nullptr, APM_E_INVALID, "apm_selftest_philox: bad arguments");
+    uint32_t* d = nullptr;
+    try {
+        HIPC(hipSetDevice(device));
+        HIPC(hipMalloc(&d, sizeof(uint32_t) * 10 * n));
+        HIPC(hipMemcpy(d, in, sizeof(uint32_t) * 6 * n, hipMemcpyHostToDevice));
+        launch_philox_test(d, d + 6 * n, n, nullptr);
+        check_launch();
+        HIPC(hipMemcpy(out, d + 6 * n, sizeof(uint32_t) * 4 * n, hipMemcpyDeviceToHost));
+        HIPC(hipFree(d));
+    } catch (const HipError& e) {
+        if (d) (void)hipFree(d);
+        return fail(nullptr, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
 int apm_prof_enable(apm_ctx* c, int on) {
     if (!c) return fail(c, APM_E_INVALID, "apm_prof_enable: null ctx");
     c->prof = on != 0;

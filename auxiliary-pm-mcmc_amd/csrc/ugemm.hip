@@ -42,6 +42,22 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
     }
 }
 
+// raw Philox4x32-10 blocks (apm_selftest_philox): in = {ctr0..3, key0, key1} per block
+__global__ __launch_bounds__(256) void k_philox_test(const uint32_t* __restrict__ in,
+                                                     uint32_t* __restrict__ out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t c[4] = {in[6 * i], in[6 * i + 1], in[6 * i + 2], in[6 * i + 3]};
+    philox4x32_10(c, in[6 * i + 4], in[6 * i + 5]);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) out[4 * i + h] = c[h];
+}
+
+void launch_philox_test(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_philox_test, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out,
+                       n);
+}
+
 __global__ __launch_bounds__(256) void k_u_normal(UPool P, const int64_t* __restrict__ ubufs,
                                                   const uint64_t* __restrict__ seeds,
                                                   const uint64_t* __restrict__ counters, int n,

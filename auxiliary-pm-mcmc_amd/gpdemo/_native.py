@@ -59,6 +59,7 @@ _SIGS = {
     'apm_prof_marker': (_i, [_p, _i]),
     'apm_prof_read': (_i, [_p, _i, _p, _p, _p, _i]),
     'apm_selftest_tile': (_i, [_i, _p, _p, _p]),
+    'apm_selftest_philox': (_i, [_i, _i64, _p, _p]),
 }
 
 _lib = None
@@ -154,6 +155,16 @@ def selftest_tile(A, B, C, device=None):
     _check(lib.apm_selftest_tile(default_device() if device is None else device, _ptr(A), _ptr(B),
                                  _ptr(C)))
     return C
+
+
+def selftest_philox(blocks, device=None):
+    """Philox4x32-10 of (counter[4], key[2]) rows (uint32) through the device round function."""
+    lib = load_library()
+    inp = np.ascontiguousarray(blocks, dtype=np.uint32).reshape(-1, 6)
+    out = np.empty((inp.shape[0], 4), dtype=np.uint32)
+    _check(lib.apm_selftest_philox(default_device() if device is None else device, inp.shape[0],
+                                   _ptr(inp), _ptr(out)))
+    return out
 
 
 # ----------------------------------------------------------------------------- context

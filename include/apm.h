@@ -135,6 +135,10 @@ int apm_prof_marker(apm_ctx *ctx, int id);
 /* C = C + A * B^T for 64x64 row-major fp64 host matrices through the f64 MFMA tile routine that
  * every Cholesky panel / trailing update uses (pins the v_mfma_f64_16x16x4 operand maps) */
 int apm_selftest_tile(int device, const double *A, const double *B, double *C);
+/* out[4i..4i+3] = Philox4x32-10(counter in[6i..6i+3], key in[6i+4..6i+5]) for i < n, through
+ * the device round function of apm_u_normal (Salmon et al., SC'11; checked against the
+ * published known-answer vectors in tests/test_gpu_kernels.py) */
+int apm_selftest_philox(int device, int64_t n, const uint32_t *in, uint32_t *out);
 
 #ifdef __cplusplus
 }

@@ -286,3 +286,58 @@ class ISEstimatorCPU(object):
                                         cached_results, K_work=self._K)
         self.n_cubic_ops += cubic
         return val, cache
+
+
+# ----------------------------------------------------------------------------- device RNG (f2)
+
+
+PHILOX_KAT = (  # Random123 kat_vectors (Salmon et al., SC'11): counter[4], key[2] -> out[4]
+    ((0, 0, 0, 0, 0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+    ((0xffffffff,) * 6, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+    ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344, 0xa4093822, 0x299f31d0),
+     (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
+)
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; Random123's philox4x32_R with R = 10)
+    on rows of uint32 counters (n, 4) and keys (n, 2): the published algorithm the batched
+    driver's device draws use (the reference draws u with numpy's MT19937 instead, so this
+    stream is pinned by the published known-answer vectors, PHILOX_KAT)."""
+    c = np.array(ctr, dtype=np.uint64).reshape(-1, 4)
+    k = np.array(key, dtype=np.uint64).reshape(-1, 2)
+    m = np.uint64(0xffffffff)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[:, 0]
+        p1 = np.uint64(0xCD9E8D57) * c[:, 2]
+        n0 = (p1 >> np.uint64(32)) ^ c[:, 1] ^ k[:, 0]
+        n2 = (p0 >> np.uint64(32)) ^ c[:, 3] ^ k[:, 1]
+        c = np.stack([n0 & m, p1 & m, n2 & m, p0 & m], 1)
+        k = np.stack([(k[:, 0] + np.uint64(0x9E3779B9)) & m,
+                      (k[:, 1] + np.uint64(0xBB67AE85)) & m], 1)
+    return c.astype(np.uint32)
+
+
+def u_normal(seed, counter, n, s):
+    """The (n, s) N(0, 1) draws of apm_u_normal for one (seed, counter) (ugemm.hip k_u_normal):
+    Philox block q = counter (q, ctr_lo, ctr_hi, q >> 32), key (seed_lo, seed_hi); its 4 words
+    give 2 Box-Muller pairs u = (w + 0.5) 2^-32 (formed in fp32 as on the device),
+    z = sqrt(-2 log u1) (cos, sin)(2 pi u2); element 4q + h. Transcendentals in float64 here
+    (the device's are fp32: compare to ~1e-6)."""
+    tot = n * s
+    q = np.arange((tot + 3) // 4, dtype=np.uint64)
+    ctr = np.stack([q & np.uint64(0xffffffff), np.full_like(q, counter & 0xffffffff),
+                    np.full_like(q, counter >> 32), q >> np.uint64(32)], 1)
+    key = np.tile(np.array([seed & 0xffffffff, seed >> 32], dtype=np.uint64), (q.shape[0], 1))
+    w = philox4x32_10(ctr, key)
+    # u exactly as the device forms it in fp32: ((float)w + 0.5f) * 2^-32
+    u = ((w.astype(np.float32) + np.float32(0.5)) * np.float32(2.3283064365386963e-10)
+         ).astype(np.float64)
+    z = np.empty((q.shape[0], 4))
+    for h in range(2):
+        r = np.sqrt(-2. * np.log(u[:, 2 * h]))
+        ang = (np.float32(6.283185307179586) * u[:, 2 * h + 1].astype(np.float32)).astype(
+            np.float64)  # the fp32 angle of the device's sincosf
+        z[:, 2 * h] = r * np.cos(ang)
+        z[:, 2 * h + 1] = r * np.sin(ang)
+    return z.reshape(-1)[:tot].reshape(n, s)

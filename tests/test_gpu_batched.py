@@ -59,3 +59,95 @@ def test_async_schedule_equals_lockstep(gpu_available, max_steps_out):
     # throughput mode: at least 2 transitions each, chains that are ahead go on
     traces2, done2 = b.run_async(2, keep_going=True)
     assert (done2 >= 2).all() and all(len(t) == d for t, d in zip(traces2, done2))
+
+
+def _data(n=150, d=4, kind='ard'):
+    from gpdemo.utils import synthetic_gp_data
+    X, y = synthetic_gp_data(n, d, 5, kind)
+    prior = dict(a_tau=1., b_tau=1. / d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    return X, y, prior
+
+
+def _current_state_consistent(smp, X, y, prior, kind='ard'):
+    """log f of every live chain = u-call at its current (slot, u) + prior, and the oracle's
+    estimate on the same (theta, fp32 u) within the estimator tolerance."""
+    kf = orc.make_kernel_func(kind, 1e-8)
+    for c in np.flatnonzero(~smp.failed):
+        lp = smp.log_prior(smp.theta[c][None])[0]
+        out, st = smp.ctx.u_eval([smp.slot_cur[c]], [smp.ub_u[c]])
+        assert st[0] == 0 and abs(out[0] + lp - smp.log_f[c]) < 1e-9 * max(1, abs(out[0]))
+        v, _, _ = orc.is_estimate(X, y, kf, smp.ctx.u_download(smp.ub_u[c]), smp.theta[c])
+        assert abs(smp.log_f[c] - (v + lp)) < 1e-3 + 2e-7 * abs(v), (c, smp.log_f[c], v + lp)
+
+
+def test_batched_ess_mh_consistent_and_batch_invariant(gpu_available):
+    """configs[1]'s sampler (APMEllSSPlusMHSampler, samplers.py:421-585) batched: consistent
+    current state (cache slot, u, log f), accepted moves, and every chain's trajectory equal
+    bit for bit to the same chain run alone (first_chain): batch composition changes nothing."""
+    from auxpm.batched import BatchedAPMEllSSPlusMHSampler
+    X, y, prior = _data()
+    th0 = np.tile(np.r_[0.0, np.full(4, np.log(2.))], (4, 1))
+    smp = BatchedAPMEllSSPlusMHSampler(X, y, 4, 16, prior, prop_scales=0.1, seed=31)
+    th, nrej = smp.get_samples(6, th0)
+    assert np.isfinite(th).all() and not smp.failed.any()
+    assert (nrej < 5).any()  # some chain accepted moves
+    _current_state_consistent(smp, X, y, prior)
+    one = BatchedAPMEllSSPlusMHSampler(X, y, 1, 16, prior, prop_scales=0.1, seed=31,
+                                       first_chain=2)
+    th1, nrej1 = one.get_samples(6, th0[2:3])
+    np.testing.assert_array_equal(th1[0], th[2])
+    assert nrej1[0] == nrej[2]
+    # adaptive phase: per-chain scales follow the accept rates
+    ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30,
+                                      lambda b, n: 1.5)
+    assert ath.shape == (4, 8, smp.P) and sc.shape == (4, 2, smp.P)
+    for c in range(4):
+        f0 = 1.5 if rates[c, 0] > 0.30 else (1 / 1.5 if rates[c, 0] < 0.15 else 1.)
+        np.testing.assert_allclose(sc[c, 0], 0.1 * f0)
+
+
+def test_batched_pmmh_laplace_phase_matches_api_sampler(gpu_available):
+    """configs[0]'s PM-MH protocol batched: the deterministic Laplace-estimator adaptive phase
+    reproduces, chain by chain and bit for bit, the API-compatible PMMHSampler driven by the GPU
+    Laplace estimator with that chain's RandomState (same proposal / uniform draw order)."""
+    import auxpm.samplers as smp_api
+    import gpdemo.estimators as est
+    import gpdemo.kernels as krn
+    import gpdemo.utils as utils
+    from auxpm.batched import BatchedPMMHSampler, chain_streams
+    X, y, prior = _data(200, 3, 'iso')
+    C = 3
+    th0 = np.array([[0.5, 0.3], [1.0, 0.8], [-0.2, 0.6]])
+    b = BatchedPMMHSampler(X, y, C, 1, prior, prop_scales=[0.5, 0.5], kernel='iso', seed=9,
+                           estimator='laplace')
+    ath, sc, rates = b.adaptive_run(th0, 5, 2, 0.15, 0.30, utils.adapt_factor_func)
+    det = est.LogMarginalLikelihoodLaplaceEstimator(X, y, krn.make_kernel_func('iso', 1e-8))
+    prngs, _ = chain_streams(9, C)
+
+    for c in range(C):
+        prng = prngs[c]
+
+        def log_f(theta):
+            return det(theta) + (utils.log_gamma_log_pdf(theta[0], prior['a_sigma'],
+                                                         prior['b_sigma']) +
+                                 utils.log_gamma_log_pdf(theta[1], prior['a_tau'], prior['b_tau']))
+        api = smp_api.PMMHSampler(
+            log_f, lambda tp, tc, s: -0.5 * np.sum(((tp - tc) / s) ** 2),
+            lambda t, s: t + s * prng.normal(size=t.shape), np.array([0.5, 0.5]), prng)
+        a_th, a_sc, a_rates = api.adaptive_run(th0[c], 5, 2, 0.15, 0.30, utils.adapt_factor_func)
+        np.testing.assert_array_equal(ath[c], a_th)
+        np.testing.assert_array_equal(sc[c], a_sc)
+        np.testing.assert_array_equal(rates[c], a_rates)
+    # main phase: IS estimator, N_imp = 1, fresh device u per proposal; consistent state
+    b.set_estimator('is')
+    th, nrej = b.get_samples(6, ath[:, -1])
+    assert np.isfinite(th).all() and not b.failed.any()
+    _current_state_consistent(b, X, y, prior, 'iso')
+    # batch invariance of the IS phase (fresh samplers: same streams for chain 1 alone)
+    b2 = BatchedPMMHSampler(X, y, C, 1, prior, prop_scales=[0.3, 0.3], kernel='iso', seed=10)
+    th2, nrej2 = b2.get_samples(6, th0)
+    one = BatchedPMMHSampler(X, y, 1, 1, prior, prop_scales=[0.3, 0.3], kernel='iso', seed=10,
+                             first_chain=1)
+    th1, nrej1 = one.get_samples(6, th0[1:2])
+    np.testing.assert_array_equal(th1[0], th2[1])
+    assert nrej1[0] == nrej2[1]

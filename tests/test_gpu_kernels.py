@@ -292,3 +292,29 @@ def test_mixed_newton_fp64_fallback(nat, monkeypatch, tol):
             assert abs(o32[b] - o64[b]) <= 1e-9 * max(1.0, abs(o64[b])), (b, o32[b], o64[b])
         else:
             np.testing.assert_allclose(f32[b], f64[b], rtol=1e-9, atol=1e-9 * np.abs(f64[b]).max())
+
+
+def test_philox_known_answers_on_device(nat):
+    """The device Philox4x32-10 round function (ugemm.hip) against the published known-answer
+    vectors and the oracle on random blocks (bit-exact, integer arithmetic)."""
+    blocks = np.array([inp for inp, _ in orc.PHILOX_KAT], dtype=np.uint32)
+    out = nat.selftest_philox(blocks)
+    np.testing.assert_array_equal(out, np.array([o for _, o in orc.PHILOX_KAT], dtype=np.uint32))
+    rnd = np.random.RandomState(3).randint(0, 2 ** 32, size=(1000, 6), dtype=np.uint64)
+    np.testing.assert_array_equal(nat.selftest_philox(rnd.astype(np.uint32)),
+                                  orc.philox4x32_10(rnd[:, :4], rnd[:, 4:]))
+
+
+def test_u_normal_matches_philox_box_muller(nat):
+    """apm_u_normal's draws for (seed, counter) are the Box-Muller transform of that Philox
+    stream (oracle.u_normal, float64) to fp32 transcendental accuracy."""
+    c = _cases()[2]
+    ctx = _ctx(nat, c)
+    n, s = c['ns1'].shape
+    seeds = [123, 2 ** 63 + 12345]
+    ctrs = [0, 2 ** 33 + 5]
+    ctx.u_normal([0, 1], seeds, ctrs)
+    for b in range(2):
+        ref = orc.u_normal(seeds[b], ctrs[b], n, s)
+        np.testing.assert_allclose(ctx.u_download(b), ref, rtol=2e-6, atol=2e-6)
+    ctx.close()

@@ -154,3 +154,10 @@ def test_pmmh_chain_fixture_consistent():
     lml, _ = orc.laplace_estimate(X, y, kf, g['theta_init'])
     assert abs(lml - float(g['calls'][0])) < 1e-8 * max(1., abs(lml))
     assert g['thetas'].shape == (30, 2) and int(g['n_adapt_calls']) == 30
+
+
+def test_philox_known_answers():
+    """The oracle's Philox4x32-10 reproduces the published known-answer vectors."""
+    for inp, out in orc.PHILOX_KAT:
+        np.testing.assert_array_equal(orc.philox4x32_10(inp[:4], inp[4:])[0],
+                                      np.array(out, dtype=np.uint32))
