@@ -136,13 +136,17 @@ def save_adaptive_run(output_dir, tag, adapt_thetas, adapt_prop_scales, adapt_ac
 
 
 def plot_trace(thetas, fig_size=(12, 8)):
-    """Trace plot of each theta component (matplotlib imported lazily)."""
+    """Trace plot of log sigma and log tau (reference utils.py:211-242): returns
+    ``(fig, ax1, ax2)`` with ax1 the log-variance and ax2 the log-length-scale axes (for ARD
+    thetas ax2 shows the first length-scale, as the reference plots column 1)."""
     import matplotlib.pyplot as plt
-    n_dim = thetas.shape[1]
-    fig, axes = plt.subplots(n_dim, 1, figsize=fig_size, squeeze=False)
-    for k in range(n_dim):
-        axes[k, 0].plot(thetas[:, k])
-        axes[k, 0].set_ylabel(r'$\theta_{{{0}}}$'.format(k))
-    axes[-1, 0].set_xlabel('Iteration')
-    fig.tight_layout()
-    return fig
+    fig = plt.figure(figsize=fig_size)
+    ax1 = fig.add_subplot(211)
+    ax1.plot(thetas[:, 0])
+    ax1.set_xlabel('Number of updates', fontsize=12)
+    ax1.set_ylabel(r'$\log\,\sigma$', fontsize=18)
+    ax2 = fig.add_subplot(212)
+    ax2.plot(thetas[:, 1])
+    ax2.set_xlabel('Number of updates', fontsize=12)
+    ax2.set_ylabel(r'$\log\,\tau$', fontsize=18)
+    return fig, ax1, ax2

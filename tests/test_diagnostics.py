@@ -41,3 +41,13 @@ def test_gelman_rubin():
     assert np.all(np.abs(r - 1) < 0.01)
     shifted = same + np.arange(4)[:, None, None]
     assert np.all(dg.gelman_rubin(shifted) > 1.5)
+
+
+def test_plot_trace_returns_reference_tuple():
+    """gpdemo.utils.plot_trace returns (fig, ax1, ax2) like the reference (utils.py:211-242)."""
+    import matplotlib
+    matplotlib.use('Agg')
+    from gpdemo.utils import plot_trace
+    fig, ax1, ax2 = plot_trace(np.random.RandomState(0).normal(size=(20, 3)))
+    assert len(ax1.lines) == 1 and len(ax2.lines) == 1
+    np.testing.assert_array_equal(ax2.lines[0].get_ydata().shape, (20,))
