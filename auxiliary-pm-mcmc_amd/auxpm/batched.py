@@ -93,6 +93,9 @@ class _BatchedChains(object):
         self.n_cubic_ops = np.zeros(C, dtype=np.int64)
         # wall seconds inside the device calls (the rest of a run is host-side sampler logic)
         self.wall = {'theta_call': 0., 'u_call': 0., 'u_draw': 0.}
+        # per theta-call: (max, mean) over its chains of the cubic-op count (IS: Newton
+        # iterations + 3) - the call's wall time follows the max, its work the mean
+        self.call_ops = []
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
@@ -115,6 +118,7 @@ class _BatchedChains(object):
         self.wall['theta_call'] += time.perf_counter() - t0
         self.n_theta_calls += len(idx)
         self.n_cubic_ops[idx] += nops
+        self.call_ops.append((int(nops.max()), float(nops.mean())))
         bad = st != 0
         if bad.any():
             self.failed[idx[bad]] = True

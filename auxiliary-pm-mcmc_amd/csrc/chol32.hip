@@ -344,6 +344,9 @@ struct __attribute__((aligned(16))) GemmSmemH3 {
 // path inside the same launch, so a chain's result does not depend on its batch. The appended
 // right-hand-side row (forward solve of W^1/2 K b, unbounded) stays fp32: super-tiles reaching
 // row tile hlim take the fp32 path.
+#ifndef H3_ABL
+#define H3_ABL 0
+#endif
 template <bool H3>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
@@ -409,6 +412,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
             brow[h] = Ab + (int64_t)(ct * 64 + (prow[h] & 63)) * A.ld + k0 * 64 + pcol[h];
         }
         auto gload = [&](int sidx, f4_t (&ra)[4], f4_t (&rb)[4]) {
+#if H3_ABL == 1  // ablation (tools/upd16_bench.cpp): every slice reads slice 0 (cache-resident)
+            sidx = 0;
+#endif
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 ra[h] = *reinterpret_cast<const f4_t*>(arow[h] + sidx * KS128);
@@ -438,6 +444,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         // lane (r16, kq): k = 8kq .. 8kq+7 of the slice = one 16-byte read per half and tile;
         // the B fragments stay in registers, the A fragments are read per tile row
         auto compute = [&](int cur) {
+#if H3_ABL == 2  // ablation: no MFMA
+            return;
+#endif
             h8_t bh[4], bl[4];
 #pragma unroll
             for (int x = 0; x < 4; ++x) {

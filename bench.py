@@ -272,6 +272,7 @@ def main():
     device_sync()  # first torch touch outside the timed region
     mark = lambda: ctx.prof_marker(1)  # noqa: E731  timed-region bracket (tools/prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
+    smp.call_ops = []
     for h in ctx.batch_hist.values():
         h.clear()
     for k in smp.wall:
@@ -414,6 +415,13 @@ def main():
         'failed_chains': int(dist.sum(int(smp.failed.sum()))),
         'newton_refinement_steps': int(dist.sum(n_refine)),
         'newton_fp64_reruns': int(dist.sum(n_rerun)),
+        'cubic_ops_per_theta_call': {
+            'mean_of_batch_max': float(np.mean([m for m, _ in smp.call_ops])) if smp.call_ops
+            else None,
+            'mean_of_batch_mean': float(np.mean([a for _, a in smp.call_ops])) if smp.call_ops
+            else None,
+            'note': 'IS: Newton iterations + 3 (estimators.py:217); a batched call lasts as long '
+                    'as its slowest chain'},
         'wall_split_s': dict(smp.wall, host_sampler=elapsed - sum(smp.wall.values())),
         'calls_by_batch_size': {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()},
         'roofline': roofline, 'cpu_baseline': cpu,
