@@ -138,6 +138,37 @@ def pmc_traffic(*kernels):
     return tot / n, os.path.relpath(files[-1], REPO)
 
 
+# flops one MFMA busy cycle of one SIMD performs (MI355X_MICROARCH.md: v_mfma_f64_16x16x4_f64 at
+# 32 FLOP/clk/SIMD, v_mfma_f32_16x16x4_f32 at 64, v_mfma_f32_16x16x32_f16 at 1024; fp16x3 counts a
+# third of its f16 flops as fp32-equivalent)
+MFMA_FLOPS_PER_BUSY_CYCLE = {'f64': 32.0, 'f32': 64.0, 'f16x3': 1024.0 / 3}
+
+
+def pmc_mfma(kind, *kernels):
+    """MFMA utilisation of the kernels (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE
+    / 8), dispatch-weighted) and the flops per dispatch those busy cycles imply, from the newest
+    committed PMC pass of this bench (profiles/r*_pmc_traffic.json 'pmc_mfma', written by
+    tools/prof_window.py). Counter runs serialise dispatches, so the utilisation is the kernel's
+    own, without the concurrent chol(K) stream."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
+    if not files:
+        return None
+    d = json.load(open(files[-1])).get('pmc_mfma', {})
+    busy = act = n = 0.0
+    for k in kernels:
+        e = d.get(k)
+        if e:
+            busy += e['mfma_busy_cycles']
+            act += e['grbm_gui_active']
+            n += e['dispatches']
+    if not n or not act:
+        return None
+    return {'util': busy / (1024.0 * act / 8.0), 'dispatches': int(n),
+            'counter_flops_per_launch': busy / n * MFMA_FLOPS_PER_BUSY_CYCLE[kind],
+            'source': os.path.relpath(files[-1], REPO)}
+
+
 def timed_region(dist, step_fn, steps, on_start=None):
     """barrier + sync, K steps, barrier + sync; returns the max over ranks of the wall time."""
     dist.barrier()
@@ -311,31 +342,36 @@ def main():
     ctx.prof_read(0, reset=True)
     _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
 
-    def mfma_roofline(name, kernel, peak, shorts):
+    def mfma_roofline(name, kernel, peak, shorts, kind):
         ms, cnt, flops = prof[name]
         if not cnt:
             return None
         avg_s = ms * 1e-3 / cnt
         achieved = (flops / cnt) / avg_s / 1e12
         tr, src = pmc_traffic(*shorts)
-        return {'kernel': kernel, 'bound': 'mfma', 'achieved': achieved, 'peak': peak,
-                'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': tr,
-                'traffic_unit': 'HBM bytes per launch', 'traffic_source': src,
-                'launches': cnt, 'avg_launch_us': avg_s * 1e6,
-                'algorithmic_flops_per_launch': flops / cnt,
-                'share_of_step_time': (ms * 1e-3) / elapsed}
+        out = {'kernel': kernel, 'bound': 'mfma', 'achieved': achieved, 'peak': peak,
+               'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': tr,
+               'traffic_unit': 'HBM bytes per launch', 'traffic_source': src,
+               'launches': cnt, 'avg_launch_us': avg_s * 1e6,
+               'algorithmic_flops_per_launch': flops / cnt,
+               'share_of_step_time': (ms * 1e-3) / elapsed}
+        mf = pmc_mfma(kind, *shorts)
+        if mf:
+            out['mfma_busy'] = dict(mf, counter_over_algorithmic_flops=mf[
+                'counter_flops_per_launch'] / (flops / cnt))
+        return out
 
     upd64 = mfma_roofline('chol_update', 'k_chol_update_t128 + k_chol_update (f64 MFMA trailing '
                           'updates of the fp64 factorisations: chol(K), SYRK + chol of '
                           'I + L_K^T W L_K)', PEAK_F64_MFMA_TFLOPS,
-                          ('k_chol_update_t128', 'k_chol_update'))
+                          ('k_chol_update_t128', 'k_chol_update'), 'f64')
     upd32 = mfma_roofline('chol_update32', 'k_chol_update32_t128 + k_chol_update32 (trailing '
                           'updates of the Newton factorisation of B, fp16x3: fp32 operands split '
                           'into fp16 hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 '
                           'accumulation; achieved in fp32-equivalent flops against the fp16 peak '
                           '/ 3)', PEAK_F16X3_TFLOPS,
                           ('k_chol_update32_t128<true>', 'k_chol_update32_t128<false>',
-                           'k_chol_update32'))
+                           'k_chol_update32'), 'f16x3')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])
@@ -361,6 +397,9 @@ def main():
                                 'traffic': tr, 'traffic_source': src, 'launches': ucnt,
                                 'avg_launch_us': ums * 1e3 / ucnt,
                                 'algorithmic_flops_per_launch': uflops / ucnt}
+        mf = pmc_mfma('f32', 'k_ugemm')
+        if mf:
+            extra['roofline_lu']['mfma_busy'] = mf
     # ESS/s on theta (Analyse results.ipynb:138-139 uses coda's effectiveSize):
     # sum over chains of min over theta components of the chain's ESS over ALL its completed
     # timed transitions, / the timed wall time. Defined for any K (the driver runs K=20); with few

@@ -98,6 +98,7 @@ def main():
             busy, act = d.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0), d.get('GRBM_GUI_ACTIVE', 0.0)
             if act > 0 and busy > 0:
                 util[k] = {'dispatches': len(disp[k]), 'mfma_busy_cycles': busy,
+                           'mfma_busy_cycles_per_dispatch': busy / len(disp[k]),
                            'grbm_gui_active': act, 'mfma_util': busy / (1024.0 * act / 8.0)}
         out['pmc_mfma'] = dict(sorted(util.items(), key=lambda x: -x[1]['mfma_busy_cycles']))
         out['pmc_mfma_formula'] = ('SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 '
