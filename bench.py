@@ -42,8 +42,8 @@ def parse():
     ap.add_argument('--steps', type=int, default=100, help='timed transitions per chain (ESS/s needs >= 100)')
     ap.add_argument('--warmup', type=int, default=20, help='untimed transitions per chain (burn-in)')
     ap.add_argument('--chains', type=int, default=64, help='chains per GPU')
-    ap.add_argument('--n', type=int, default=4096)
-    ap.add_argument('--d', type=int, default=32)
+    ap.add_argument('--n', '--n-data', dest='n', type=int, default=4096)
+    ap.add_argument('--d', '--n-features', dest='d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
     ap.add_argument('--schedule', choices=('async', 'lockstep'), default='async',
@@ -96,6 +96,12 @@ class Dist(object):
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
+
+
+def rank_device(dist):
+    """GPU of this rank: LOCAL_RANK (one process per GPU); APM_DEVICE pins every rank to one
+    device instead (the 2-rank rehearsal of the N>1 path on a 1-GPU box, tests/test_gpu_dist.py)."""
+    return int(os.environ.get('APM_DEVICE', dist.local_rank))
 
 
 def chain_seed(base, rank):
@@ -287,7 +293,7 @@ def main():
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
-        seed=chain_seed(a.seed, dist.rank), device=dist.local_rank)
+        seed=chain_seed(a.seed, dist.rank), device=rank_device(dist))
     P = smp.P
     smp.initialise()
     if a.schedule == 'async':
