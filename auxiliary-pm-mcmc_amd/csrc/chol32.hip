@@ -1008,8 +1008,9 @@ __global__ __launch_bounds__(256) void k_nan_fill(double* out, int64_t vstride, 
 template <bool FWD>
 __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* Dinv,
                                                    int64_t dstride, const double* r, double* out,
-                                                   int64_t vstride, Live live, int fail_code) {
-    const int b = blockIdx.x / TRM_G, g = blockIdx.x % TRM_G;
+                                                   int64_t vstride, Live live, int fail_code,
+                                                   int G) {
+    const int b = blockIdx.x / G, g = blockIdx.x % G;
     if (!live32(live, b)) return;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row = t >> 2, q = t & 3;  // tile row, 16-column quarter
@@ -1047,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
         return *reinterpret_cast<const f4_t*>(Lb + o);
     };
     int have = 0;  // solve-order blocks [0, have) are in LDS
-    for (int s = g; s < nb; s += TRM_G) {
+    for (int s = g; s < nb; s += G) {
         const int J = blk(s);
         double acc[16];
 #pragma unroll
@@ -1070,14 +1071,52 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
                     for (int e = 0; e < 4; ++e) acc[4 * u + e] = fma((double)v[u][e], x, acc[4 * u + e]);
             }
         };
-        // all earlier blocks but the previous step's, then that one
+        // all earlier blocks but the previous step's, then that one; the early tiles stream with
+        // two tiles' loads in flight ahead of the one being consumed (the step's critical path
+        // is this one workgroup's read of its block row)
         const int early = s > 0 ? s - 1 : 0;
         if (have < early) {
             fetch(have, early);
             have = early;
         }
         __syncthreads();
-        for (int idx = 0; idx < early; ++idx) consume(blk(idx));
+        {
+            f4_t p0[4], p1[4], p2[4];
+            auto ld4 = [&](f4_t (&v)[4], int idx) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = piece(J, blk(idx), u);
+            };
+            auto use = [&](const f4_t (&v)[4], int I) {
+                if (FWD) {
+                    const double* x = xs + I * 64 + 16 * q;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[0] = fma((double)v[u][e], x[4 * u + e], acc[0]);
+                } else {
+                    const double x = xs[I * 64 + row];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[4 * u + e] = fma((double)v[u][e], x, acc[4 * u + e]);
+                }
+            };
+            if (early > 0) ld4(p0, 0);
+            if (early > 1) ld4(p1, 1);
+            int idx = 0;
+            for (; idx + 2 < early; idx += 3) {  // same order of accumulation as one at a time
+                ld4(p2, idx + 2);
+                use(p0, blk(idx));
+                if (idx + 3 < early) ld4(p0, idx + 3);
+                use(p1, blk(idx + 1));
+                if (idx + 4 < early) ld4(p1, idx + 4);
+                use(p2, blk(idx + 2));
+            }
+            if (idx < early) use(p0, blk(idx));
+            if (idx + 1 < early) use(p1, blk(idx + 1));
+        }
         if (s > 0) {
             if (have < s) {
                 fetch(s - 1, s);
@@ -1145,14 +1184,19 @@ void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstri
         attr = true;
     }
     const int np = nb * 64;
+    static int G = 0;
+    if (!G) {  // workgroups per chain (APM_TRSV_G, development knob)
+        const char* e = getenv("APM_TRSV_G");
+        G = e ? std::max(1, std::min(16, atoi(e))) : TRM_G;
+    }
     hipLaunchKernelGGL(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,
                        np, live);
     if (fwd)
-        hipLaunchKernelGGL(k_trsv32_mw<true>, dim3(nchains * TRM_G), dim3(256), lds, s, A, nb,
-                           Dinv, dstride, r, out, vstride, live, fail_code);
+        hipLaunchKernelGGL(k_trsv32_mw<true>, dim3(nchains * G), dim3(256), lds, s, A, nb,
+                           Dinv, dstride, r, out, vstride, live, fail_code, G);
     else
-        hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * TRM_G), dim3(256), lds, s, A, nb,
-                           Dinv, dstride, r, out, vstride, live, fail_code);
+        hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * G), dim3(256), lds, s, A, nb,
+                           Dinv, dstride, r, out, vstride, live, fail_code, G);
 }
 
 static size_t trf_lds_bytes(int nb) {

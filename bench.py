@@ -110,11 +110,16 @@ def chain_seed(base, rank):
     return base + 7919 * rank
 
 
+_SYNC_DEVICE = [None]
+
+
 def device_sync():
+    """torch.cuda.synchronize() on this rank's GPU (not on device 0 for every rank); the
+    library's own calls are synchronous already, this brackets the timed region."""
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(_SYNC_DEVICE[0])
     except Exception:
         pass
 
@@ -289,6 +294,7 @@ def main():
     from gpdemo import _native
     from gpdemo.utils import synthetic_gp_data
 
+    _SYNC_DEVICE[0] = rank_device(dist)
     X, y = synthetic_gp_data(a.n, a.d, a.seed)
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
