@@ -74,7 +74,7 @@ struct apm_ctx {
     // otherwise every K x product uses the symmetric lower-tile kernel (launch_symv)
     bool k_full = false;
     // profiling
-    bool prof = false;
+    int prof = 0;  // apm_prof_enable level
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<ProfRec> recs;
@@ -157,16 +157,20 @@ struct ProfScope {
     double work;
     hipStream_t s;
     hipEvent_t a{}, b{};
+    bool on = false;
     ProfScope(apm_ctx* c_, int k, double w, hipStream_t s_ = nullptr)
         : c(c_), kind(k), work(w), s(s_ ? s_ : c_->stream) {
-        if (c->prof && kind >= 0) {
+        // the all-updates kinds time every in-panel launch: detailed level (2) only
+        const bool all_upd = kind == APM_PROF_CHOL_UPDATE || kind == APM_PROF_CHOL_UPDATE32;
+        if (kind >= 0 && c->prof >= (all_upd ? 2 : 1)) {
+            on = true;
             a = next_event(c);
             b = next_event(c);
             HIPC(hipEventRecord(a, s));
         }
     }
     ~ProfScope() {
-        if (c->prof && kind >= 0 && hipEventRecord(b, s) == hipSuccess)
+        if (on && hipEventRecord(b, s) == hipSuccess)
             c->recs.push_back(ProfRec{a, b, kind, work});
     }
 };
@@ -1382,7 +1386,7 @@ int apm_selftest_philox(int device, int64_t n, const uint32_t* in, uint32_t* out
 
 int apm_prof_enable(apm_ctx* c, int on) {
     if (!c) return fail(c, APM_E_INVALID, "apm_prof_enable: null ctx");
-    c->prof = on != 0;
+    c->prof = on < 0 ? 0 : (on > 2 ? 2 : on);
     return APM_SUCCESS;
 }
 

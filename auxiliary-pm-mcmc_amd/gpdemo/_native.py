@@ -18,7 +18,7 @@ KERNEL_ISO, KERNEL_ARD, KERNEL_PRECOMPUTED = 0, 1, 2
 EST_IS, EST_PRIORMC, EST_LAPLACE = 0, 1, 2
 STATUS_OK, STATUS_CHOL_K, STATUS_CHOL_B, STATUS_CHOL_C, STATUS_MAXITER = 0, 1, 2, 3, 4
 PROF_GRAM, PROF_CHOL_UPDATE, PROF_UGEMM, PROF_CHOL_UPDATE32, PROF_STATS = 0, 1, 2, 3, 4
-PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER = 5, 6
+PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER, PROF_NKINDS = 5, 6, 7
 
 
 class NativeUnavailableError(RuntimeError):
@@ -312,7 +312,8 @@ class Context(object):
 
     # --- profiling
     def prof_enable(self, on=True):
-        _check(self.lib.apm_prof_enable(self._h, int(bool(on))), self._h)
+        """on: False/0 off, True/1 the roofline kinds, 2 every kind (apm.h)."""
+        _check(self.lib.apm_prof_enable(self._h, int(on)), self._h)
 
     def prof_marker(self, marker_id):
         _check(self.lib.apm_prof_marker(self._h, int(marker_id)), self._h)

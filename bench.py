@@ -309,9 +309,11 @@ def main():
         for _ in range(a.warmup):
             smp.step()
     ctx = smp.ctx
-    for k in (0, 1, 2, 3, 4):
+    for k in range(_native.PROF_NKINDS):
         ctx.prof_read(k, reset=True)
-    ctx.prof_enable(True)
+    # roofline level: one HIP-event pair per Gram, L.U and rank-512 update launch (the in-panel
+    # update launches are not bracketed: their events cost ~2 % of the theta-call)
+    ctx.prof_enable(1)
     device_sync()  # first torch touch outside the timed region
     mark = lambda: ctx.prof_marker(1)  # noqa: E731  timed-region bracket (tools/prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
@@ -349,7 +351,9 @@ def main():
     n_u = (smp.n_u_calls - u0) / max(1, local_tr)
 
     prof = {}
-    for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32')):
+    for k, name in ((_native.PROF_GRAM, 'gram'), (_native.PROF_CHOL_UPDATE_OUTER, 'chol_update'),
+                    (_native.PROF_UGEMM, 'ugemm'),
+                    (_native.PROF_CHOL_UPDATE32_OUTER, 'chol_update32')):
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
     _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
@@ -373,17 +377,16 @@ def main():
                 'counter_flops_per_launch'] / (flops / cnt))
         return out
 
-    upd64 = mfma_roofline('chol_update', 'k_chol_update_t128 + k_chol_update (f64 MFMA trailing '
-                          'updates of the fp64 factorisations: chol(K), SYRK + chol of '
-                          'I + L_K^T W L_K)', PEAK_F64_MFMA_TFLOPS,
-                          ('k_chol_update_t128', 'k_chol_update'), 'f64')
-    upd32 = mfma_roofline('chol_update32', 'k_chol_update32_t128 + k_chol_update32 (trailing '
-                          'updates of the Newton factorisation of B, fp16x3: fp32 operands split '
-                          'into fp16 hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 '
-                          'accumulation; achieved in fp32-equivalent flops against the fp16 peak '
-                          '/ 3)', PEAK_F16X3_TFLOPS,
-                          ('k_chol_update32_t128<true>', 'k_chol_update32_t128<false>',
-                           'k_chol_update32'), 'f16x3')
+    upd64 = mfma_roofline('chol_update', 'k_chol_update_t128 (f64 MFMA rank-512 trailing updates '
+                          'of the fp64 factorisations: chol(K), the single-launch SYRK and the '
+                          'chol of I + L_K^T W L_K)', PEAK_F64_MFMA_TFLOPS,
+                          ('k_chol_update_t128',), 'f64')
+    upd32 = mfma_roofline('chol_update32', 'k_chol_update32_t128 (rank-512 trailing updates of '
+                          'the Newton factorisation of B, fp16x3: fp32 operands split into fp16 '
+                          'hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 accumulation; '
+                          'achieved in fp32-equivalent flops against the fp16 peak / 3)',
+                          PEAK_F16X3_TFLOPS,
+                          ('k_chol_update32_t128<true>', 'k_chol_update32_t128<false>'), 'f16x3')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])

@@ -121,6 +121,9 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
 #define APM_PROF_CHOL_UPDATE32_OUTER 5 /* the rank-64*OUTER launches among CHOL_UPDATE32 */
 #define APM_PROF_CHOL_UPDATE_OUTER 6   /* the rank-64*OUTER launches among CHOL_UPDATE */
 #define APM_PROF_NKINDS 7
+/* on = 0 off; 1 the roofline kinds (GRAM, UGEMM and the two *_OUTER kinds: one event pair per
+ * launch of those kernels only, so that the timing adds little to a timed region); 2 every kind
+ * (CHOL_UPDATE / CHOL_UPDATE32 add an event pair around every in-panel update launch) */
 int apm_prof_enable(apm_ctx *ctx, int on);
 /* total device milliseconds and launch count per tracked kernel since the last reset; also the
  * algorithmic work: bytes (GRAM) or flops (CHOL_UPDATE, CHOL_UPDATE32 = the fp32 Newton

@@ -83,7 +83,7 @@ def main():
         if r == a.reps - 1:
             for k in range(5):
                 ctx.prof_read(k, reset=True)
-            ctx.prof_enable(True)
+            ctx.prof_enable(2)
         t0 = time.perf_counter()
         out, st, nops = ctx.theta_eval(_native.EST_IS, th, idx, idx)
         t1 = time.perf_counter()

@@ -18,6 +18,7 @@ ap.add_argument('--d', type=int, default=32)
 ap.add_argument('--s', type=int, default=256)
 ap.add_argument('--batch', type=int, default=1)
 ap.add_argument('--reps', type=int, default=3)
+ap.add_argument('--no-prof', action='store_true')
 a = ap.parse_args()
 
 X, y = utils.synthetic_gp_data(a.n, a.d, 20151009)
@@ -27,10 +28,10 @@ ctx.u_normal(np.arange(a.batch), np.full(a.batch, 7), np.arange(a.batch))
 th = np.tile(np.r_[0.0, np.full(a.d, np.log(np.sqrt(a.d)))], (a.batch, 1))
 th += np.random.RandomState(0).normal(scale=0.1, size=th.shape)
 for r in range(a.reps):
-    if r == min(1, a.reps - 1):  # rep 0 is cold (tile lists, first launches): not profiled
+    if r == min(1, a.reps - 1) and not a.no_prof:  # rep 0 is cold (tile lists, first launches): not profiled
         for k in range(7):
             ctx.prof_read(k, reset=True)
-        ctx.prof_enable(True)
+        ctx.prof_enable(2)
     t0 = time.perf_counter()
     out, st, nops = ctx.theta_eval(_native.EST_IS, th, np.arange(a.batch), np.arange(a.batch))
     t1 = time.perf_counter()
