@@ -89,6 +89,10 @@ struct apm_ctx {
     bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
+    // dataflow in-panel factorisation of the Newton matrix (APM_DF32=0: the launch sequence)
+    bool df32 = true;
+    unsigned long long* dfprog = nullptr;  // per (chain, row tile) progress words
+    unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
     // previous convergence read; update_flops x live_n instead of x count)
     int live_n = 0;
@@ -368,8 +372,27 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
+    const bool df = c->df32 && c->fuse_diag && c->left_inner && OUTER32 <= 14;
+    const unsigned long long fact = ++c->df_fact;
     for (int K = k0; K < k1; K += OUTER32) {
         const int Kend = std::min(K + OUTER32, k1);
+        if (df) {  // the same steps in one dataflow launch per outer panel (chol32.hip)
+            if (!have_diag) {
+                launch_chol_diag32(M, K, D, ds, c->ldet, c->lstride, lv, fail_code, count,
+                                   c->stream);
+                check_launch();
+            }
+            launch_chol_panel_df32(M, K, Kend - K, R,
+                                   FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
+                                   count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
+                                   (fact << 16) | ((unsigned long long)(K / OUTER32) << 4),
+                                   c->stream);
+            check_launch();
+            have_diag = Kend < k1;
+            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
+                             fail_code);
+            continue;
+        }
         if (c->fuse_diag && c->left_inner) {  // left-looking inside the panel (chol_range)
             for (int k = K; k < Kend; ++k) {
                 if (k > K)
@@ -869,6 +892,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_TRSV_MW")) c->trsv_mw = atoi(e) != 0;
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
+    if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -934,6 +958,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->d_ubufs = c->d_slots + B;
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 44, hipHostMallocDefault));
     c->h3ok = dalloc<int>(c, B);
+    c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1));
+    HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * B * (c->nb + 1)));
     // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:
     // [i3: 3B int64][ca: B][cb: B][seeds: B][ctrs: B]
     c->d_i3 = dalloc<int64_t>(c, 7 * B);

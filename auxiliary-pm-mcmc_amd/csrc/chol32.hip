@@ -309,6 +309,222 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
                        ntiles, nchains, live, fd, hlim, h3ok);
 }
 
+// ------------------------------------------------------------------ dataflow in-panel factorisation
+// One launch factors the tile columns [K, K + ncols) of an outer panel (the diagonal tile (K, K)
+// already factored): workgroup (row tile i, chain b) walks its row through the panel's columns,
+// for column k the left-looking update A_ik -= L_i[K:k] L_k[K:k]^T (the in-panel k_chol_update32
+// step, same operands, same code) and then either the diagonal factorisation (i == k; diag.h) or
+// the panel TRSM A_ik <- A_ik inv(L_kk)^T (k_chol_panel32's product, same accumulation order).
+// Results are bitwise those of the launch sequence it replaces (2 launches per column), whose
+// dependent-launch boundaries and the diagonal tile's latency at the tail of every update launch
+// were ~110 us per column.
+//
+// Row k's progress is a per-(chain, row) word: base + s after s of its columns are final
+// (base = factorisation and panel, monotonic, so no reset between launches; s = 15: the chain
+// failed, waiters leave). A row waits for row k (k < i, lower workgroup index) before its update
+// of column k (s >= k-K: L_k[K:k] final) and before the TRSM (s >= k-K+1: L_kk and inv(L_kk)
+// final). Only the diagonal-block rows publish; their tiles are stored write-through (sc1) and
+// drained before one lane's agent-scope flag store; a waiter polls relaxed (one lane, s_sleep),
+// then one agent-scope acquire (MI355X_MICROARCH.md, inter-workgroup visibility). Workgroups
+// depend only on lower indices (row-major over (row, chain)), so in-order dispatch guarantees
+// progress; a bounded spin marks the chain failed instead of hanging (the Newton loop then reruns
+// it in fp64).
+#define DF_FAILED 15
+#define DF_SPIN (1 << 22)
+__device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float* T, int64_t ld,
+                                                 int wr, int wc, int lane) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                __hip_atomic_store(T + (int64_t)(32 * wr + 16 * bi + F32_CROW(lane, r)) * ld +
+                                       32 * wc + 16 * bj + (lane & 15),
+                                   acc[bi][bj][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
+                                                         FusedDiag<float> fd, Live live, int hlim,
+                                                         const int* __restrict__ h3ok,
+                                                         unsigned long long* prog,
+                                                         int64_t pstride,
+                                                         unsigned long long base) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
+    __shared__ union {
+        GemmSmem32 g;
+        DiagSmem32 d;
+    } sm;
+    __shared__ unsigned long long seen;
+    const int b = (int)(blockIdx.x % nchains);
+    const int i = K + (int)(blockIdx.x / nchains);
+    const int Kend = K + ncols;
+    const bool pub = i < Kend;  // rows of the diagonal block: later rows wait on them
+    unsigned long long* pr = prog + b * pstride;
+    auto publish = [&](unsigned long long v) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores drained
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(pr + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // one lane polls row k's word relaxed, then ONE agent acquire for the workgroup; false: the
+    // chain failed (or the spin bound was hit)
+    auto wait_row = [&](int k, unsigned long long need) -> bool {
+        if (threadIdx.x == 0) {
+            unsigned long long v =
+                __hip_atomic_load(pr + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int spins = 0; v < need; ++spins) {
+                if (spins > DF_SPIN) {
+                    v = base + DF_FAILED;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+                v = __hip_atomic_load(pr + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            seen = v;
+        }
+        __syncthreads();
+        return (seen & 15) != DF_FAILED;
+    };
+    auto leave_failed = [&]() {
+        if (threadIdx.x == 0) live.status[b] = fd.fail_code;
+        if (pub) publish(base + DF_FAILED);
+    };
+    if (!live32(live, b)) {
+        if (pub) publish(base + DF_FAILED);
+        return;
+    }
+    if (i == K) return;  // (K, K) was factored by the launch before
+    float* Ab = A.base + b * A.cstride;
+    const bool h3 = i < hlim && (!h3ok || h3ok[b]);
+    const int last = min(Kend - 1, i);
+    for (int k = K; k <= last; ++k) {
+        const int c = k - K;
+        float* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
+        f4_t acc[2][2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+        if (c > 0) {  // left-looking update by the panel's earlier columns (k_chol_update32)
+            if (i != k) {
+                if (!wait_row(k, base + c)) {
+                    leave_failed();
+                    return;
+                }
+            } else {  // own earlier tiles only: refresh this CU's L1 (they were re-stored)
+                if (threadIdx.x == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+            }
+            if (h3)
+                tile_gemm_nt32<true, true>(acc, Ab + (int64_t)(i * 64) * A.ld + K * 64, A.ld,
+                                           Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c,
+                                           sm.g, Aik, A.ld);
+            else
+                tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + K * 64, A.ld,
+                                     Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c, sm.g,
+                                     Aik, A.ld);
+        } else {
+            tile32_load(acc, Aik, A.ld, wr, wc, lane);
+        }
+        if (i == k) {  // diagonal tile: factor and publish (row i is then done)
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        sm.d.T[(32 * wr + 16 * bi + F32_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
+                               (lane & 15)] = acc[bi][bj][r];
+            __syncthreads();
+            if (wv == 0) {
+                const bool ok = diag_compute<true, float>(sm.d, lane);
+                if (lane == 0) sm.d.ok = ok;
+            }
+            __syncthreads();
+            if (!sm.d.ok) {
+                leave_failed();
+                return;
+            }
+            diag_store<float, float, true>(sm.d, Aik, A.ld,
+                                           fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
+                                           fd.ldet + b * fd.lstride + i, threadIdx.x, 256);
+            publish(base + c + 1);
+            return;
+        }
+        // panel TRSM: A_ik inv(L_kk)^T, the updated tile and inv(L_kk) staged as k_chol_panel32's
+        // two 32-deep slices (A operand: acc; B operand: inv(L_kk) row-major)
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sm.g.a[wc][32 * wr + 16 * bi + F32_CROW(lane, r)][16 * bj + (lane & 15)] =
+                        acc[bi][bj][r];
+        // inv(L_KK) comes from the launch before; later columns' from row k's workgroup
+        if (c > 0 && !wait_row(k, base + c + 1)) {
+            leave_failed();
+            return;
+        }
+        {
+            const float* D = fd.Dinv + b * fd.dstride + (int64_t)k * 4096;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int p = threadIdx.x + 256 * h;  // 16-byte piece: row p / 16, column 4 (p % 16)
+                const int row = p >> 4, col = 4 * (p & 15);
+                const f4_t v = *reinterpret_cast<const f4_t*>(D + row * 64 + col);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sm.g.b[col >> 5][row][(col & 31) + e] = v[e];
+            }
+        }
+        __syncthreads();
+        f4_t x[2][2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) x[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+        const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll
+        for (int cur = 0; cur < 2; ++cur)
+#pragma unroll
+            for (int t = 0; t < KS32 / 4; ++t) {
+                float a[2], bb[2];
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi) a[bi] = sm.g.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj) bb[bj] = sm.g.b[cur][32 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 2; ++bj)
+                        x[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj], x[bi][bj],
+                                                                        0, 0, 0);
+            }
+        if (pub) {
+            tile32_store_sc1(x, Aik, A.ld, wr, wc, lane);
+            publish(base + c + 1);
+        } else {
+            tile32_store(x, Aik, A.ld, wr, wc, lane);
+            __syncthreads();  // the staging area is reused by the next column's update
+        }
+    }
+}
+
+void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
+                            int nchains, int hlim, const int* h3ok, unsigned long long* prog,
+                            int64_t pstride, unsigned long long base, hipStream_t s) {
+    if (ncols < 2 || ncols > 14 || R - K <= 1) return;  // column K alone: nothing to do here
+    const long total = (long)(R - K) * nchains;
+    hipLaunchKernelGGL(k_chol_panel_df32, dim3((unsigned)total), dim3(256), 0, s, A, K, ncols,
+                       nchains, fd, live, hlim, h3ok, prog, pstride, base);
+}
+
 // ------------------------------------------------------------------------- 128x128 trailing update
 // The rank-64*kc outer updates with one 128x128 super-tile (2x2 tiles) per workgroup: each wave
 // owns a 64x64 tile (4x4 v_mfma_f32_16x16x4_f32 accumulators), so a slice of operands staged in

@@ -358,8 +358,9 @@ __device__ bool diag_compute(DiagSmemT<R>& S, int lane) {
 
 // Stores of a factored tile by `nthr` threads (64: one wave; 256: the fused update's workgroup):
 // L (zeros above the diagonal) to At, inv(L) row-major to D (16-byte stores), sum(log diag L)
-// to *ldet_out (wave 0).
-template <class TS, class R = double>
+// to *ldet_out (wave 0). SC1 (fp32 tiles only): L and inv(L) stored write-through (8-byte
+// agent-scope stores) for a hand-off to other workgroups inside the launch (k_chol_panel_df32).
+template <class TS, class R = double, bool SC1 = false>
 __device__ void diag_store(DiagSmemT<R>& S, TS* At, int64_t ld, TS* D, double* ldet_out, int tid,
                            int nthr) {
     const R* T = S.T;
@@ -373,6 +374,15 @@ __device__ void diag_store(DiagSmemT<R>& S, TS* At, int64_t ld, TS* D, double* l
         if constexpr (sizeof(TS) == 8) {
             *reinterpret_cast<d2_t*>(At + (int64_t)q * ld + p2) = d2_t{l0, l1};
             *reinterpret_cast<d2_t*>(D + q * 64 + p2) = d2_t{x0, x1};
+        } else if constexpr (SC1) {
+            const float2 lv{(float)l0, (float)l1}, xv{(float)x0, (float)x1};
+            unsigned long long lu, xu;
+            __builtin_memcpy(&lu, &lv, 8);
+            __builtin_memcpy(&xu, &xv, 8);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(At + (int64_t)q * ld + p2), lu,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(D + q * 64 + p2), xu,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             *reinterpret_cast<float2*>(At + (int64_t)q * ld + p2) = float2{(float)l0, (float)l1};
             *reinterpret_cast<float2*>(D + q * 64 + p2) = float2{(float)x0, (float)x1};

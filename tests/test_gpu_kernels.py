@@ -272,6 +272,27 @@ def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
         assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
 
 
+def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch):
+    """The Newton factor's in-panel steps as one dataflow launch per outer panel
+    (k_chol_panel_df32, default) against the per-column launch sequence (APM_DF32=0): same
+    operands, same accumulation order, so modes, estimates, statuses and iteration counts are
+    bitwise equal - also for a batch with a chain at an extreme theta (fp32 operands, possibly a
+    failed fp32 factorisation and its fp64 rerun) next to ordinary ones, at three outer panels."""
+    X, y, thetas, ns = _mixed_case(n=1100)
+    ext = thetas[0].copy()
+    ext[0] = 45.0
+    thetas = np.vstack([thetas, ext])
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    np.testing.assert_array_equal(s1, s0)
+    np.testing.assert_array_equal(n1, n0)
+    assert (s0[:3] == 0).all()
+    for b in range(len(thetas)):
+        if s0[b] == 0:
+            np.testing.assert_array_equal(f1[b], f0[b])
+            assert o1[b] == o0[b]
+
+
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
 def test_mixed_newton_fp64_fallback(nat, monkeypatch, tol):
     """Chains whose refined fp32 solve fails the acceptance test are rerun in fp64 from f = 0
