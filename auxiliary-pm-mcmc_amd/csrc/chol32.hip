@@ -1266,27 +1266,23 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
     int have = 0;  // solve-order blocks [0, have) are in LDS
     for (int s = g; s < nb; s += G) {
         const int J = blk(s);
+        // the step's critical-path operands, independent of the solution: the previous step's
+        // tile and this thread's 16 entries of inv(L_JJ), loaded before any wait
+        f4_t plast[4];
+        if (s > 0) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) plast[u] = piece(J, blk(s - 1), u);
+        }
+        float dreg[16];
+        {
+            const float* D = Db + (int64_t)J * 4096;
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                dreg[e] = FWD ? D[row * 64 + 16 * q + e] : D[(16 * q + e) * 64 + row];
+        }
         double acc[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) acc[c] = 0.0;
-        auto consume = [&](int I) {
-            f4_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = piece(J, I, u);
-            if (FWD) {
-                const double* x = xs + I * 64 + 16 * q;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[0] = fma((double)v[u][e], x[4 * u + e], acc[0]);
-            } else {
-                const double x = xs[I * 64 + row];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[4 * u + e] = fma((double)v[u][e], x, acc[4 * u + e]);
-            }
-        };
         // all earlier blocks but the previous step's, then that one; the early tiles stream with
         // two tiles' loads in flight ahead of the one being consumed (the step's critical path
         // is this one workgroup's read of its block row)
@@ -1332,14 +1328,14 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
             }
             if (idx < early) use(p0, blk(idx));
             if (idx + 1 < early) use(p1, blk(idx + 1));
-        }
-        if (s > 0) {
-            if (have < s) {
-                fetch(s - 1, s);
-                have = s;
+            if (s > 0) {
+                if (have < s) {
+                    fetch(s - 1, s);
+                    have = s;
+                }
+                __syncthreads();
+                use(plast, blk(s - 1));
             }
-            __syncthreads();
-            consume(blk(s - 1));
         }
         if (FWD) {
             double sum = acc[0];
@@ -1365,13 +1361,9 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
         // x_J[c] = sum_m inv(L_JJ)[c][m] rj[m] (FWD) or inv(L_JJ)[m][c] rj[m] (BWD): thread (c, q)
         // sums m = 16q .. 16q+15
         {
-            const float* D = Db + (int64_t)J * 4096;
             double sum = 0.0;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = 16 * q + e;
-                sum = fma((double)(FWD ? D[row * 64 + m] : D[m * 64 + row]), rj[m], sum);
-            }
+            for (int e = 0; e < 16; ++e) sum = fma((double)dreg[e], rj[16 * q + e], sum);
             sum += __shfl_xor(sum, 1, 64);
             sum += __shfl_xor(sum, 2, 64);
             if (q == 0) {
