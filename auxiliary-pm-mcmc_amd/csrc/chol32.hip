@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
 void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base, hipStream_t s) {
-    if (ncols < 2 || ncols > 14 || R - K <= 1) return;  // column K alone: nothing to do here
+    if (ncols < 1 || ncols > 14 || R - K <= 1) return;  // (one column: its panel TRSM)
     const long total = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32, dim3((unsigned)total), dim3(256), 0, s, A, K, ncols,
                        nchains, fd, live, hlim, h3ok, prog, pstride, base);

@@ -272,13 +272,15 @@ def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
         assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
 
 
-def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch):
+@pytest.mark.parametrize('n', [560, 1100])
+def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch, n):
     """The Newton factor's in-panel steps as one dataflow launch per outer panel
     (k_chol_panel_df32, default) against the per-column launch sequence (APM_DF32=0): same
     operands, same accumulation order, so modes, estimates, statuses and iteration counts are
     bitwise equal - also for a batch with a chain at an extreme theta (fp32 operands, possibly a
-    failed fp32 factorisation and its fp64 rerun) next to ordinary ones, at three outer panels."""
-    X, y, thetas, ns = _mixed_case(n=1100)
+    failed fp32 factorisation and its fp64 rerun) next to ordinary ones; n = 560: a last outer
+    panel of one column (its TRSM only), n = 1100: three outer panels."""
+    X, y, thetas, ns = _mixed_case(n=n)
     ext = thetas[0].copy()
     ext[0] = 45.0
     thetas = np.vstack([thetas, ext])
