@@ -400,6 +400,15 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
     float* Ab = A.base + b * A.cstride;
     const bool h3 = i < hlim && (!h3ok || h3ok[b]);
     const int last = min(Kend - 1, i);
+    // the diagonal tile's update by all but the last of its row's panel columns, accumulated at
+    // the step before (off the diagonal chain); the step itself adds the last column's slices and
+    // the old tile - the same slices in the same order as one call over the whole depth
+    f4_t dacc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) dacc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const float* Ai = Ab + (int64_t)(i * 64) * A.ld;
     for (int k = K; k <= last; ++k) {
         const int c = k - K;
         float* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
@@ -421,14 +430,34 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
                 }
                 __syncthreads();
             }
-            if (h3)
-                tile_gemm_nt32<true, true>(acc, Ab + (int64_t)(i * 64) * A.ld + K * 64, A.ld,
+            if (i == k) {  // the diagonal tile: its last column's slices and the old tile
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = dacc[bi][bj];
+                if (h3)
+                    tile_gemm_nt32<true, true>(acc, Ai + (k - 1) * 64, A.ld, Ai + (k - 1) * 64,
+                                               A.ld, 64, sm.g, Aik, A.ld);
+                else
+                    tile_gemm_nt32<true>(acc, Ai + (k - 1) * 64, A.ld, Ai + (k - 1) * 64, A.ld,
+                                         64, sm.g, Aik, A.ld);
+            } else if (h3) {
+                tile_gemm_nt32<true, true>(acc, Ai + K * 64, A.ld,
                                            Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c,
                                            sm.g, Aik, A.ld);
-            else
-                tile_gemm_nt32<true>(acc, Ab + (int64_t)(i * 64) * A.ld + K * 64, A.ld,
+            } else {
+                tile_gemm_nt32<true>(acc, Ai + K * 64, A.ld,
                                      Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c, sm.g,
                                      Aik, A.ld);
+            }
+            if (k + 1 == i) {  // next step is the diagonal tile: its columns K .. k-1 now
+                if (h3)
+                    tile_gemm_nt32<true, true>(dacc, Ai + K * 64, A.ld, Ai + K * 64, A.ld, 64 * c,
+                                               sm.g, nullptr, 0);
+                else
+                    tile_gemm_nt32<true>(dacc, Ai + K * 64, A.ld, Ai + K * 64, A.ld, 64 * c, sm.g,
+                                         nullptr, 0);
+            }
         } else {
             tile32_load(acc, Aik, A.ld, wr, wc, lane);
         }
