@@ -331,6 +331,25 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 // it in fp64).
 #define DF_FAILED 15
 #define DF_SPIN (1 << 22)
+// DF_TRACE (diagnostic builds only, tools/df_trace.py): wall-clock stamps of chain 0's first
+// outer panel, [row - K][column - K][event], read back by apm_debug_df_trace
+#ifdef DF_TRACE
+__device__ unsigned long long df_trace[64 * 16 * 8];
+#define DF_STAMP(ev)                                                                         \
+    do {                                                                                     \
+        if (b == 0 && K == 0 && threadIdx.x == 0 && i - K < 64)                              \
+            __hip_atomic_store(&df_trace[((i - K) * 16 + (k - K)) * 8 + (ev)],                \
+                               (unsigned long long)__builtin_amdgcn_s_memrealtime(),         \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                  \
+    } while (0)
+extern "C" int apm_debug_df_trace(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(df_trace), sizeof(df_trace)) == hipSuccess ? 0 : 1;
+}
+#else
+#define DF_STAMP(ev) \
+    do {             \
+    } while (0)
+#endif
 __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float* T, int64_t ld,
                                                  int wr, int wc, int lane) {
 #pragma unroll
@@ -411,6 +430,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
     const float* Ai = Ab + (int64_t)(i * 64) * A.ld;
     for (int k = K; k <= last; ++k) {
         const int c = k - K;
+        DF_STAMP(0);
         float* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
         f4_t acc[2][2];
 #pragma unroll
@@ -423,6 +443,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
                     leave_failed();
                     return;
                 }
+                DF_STAMP(1);
             } else {  // own earlier tiles only: refresh this CU's L1 (they were re-stored)
                 if (threadIdx.x == 0) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -461,6 +482,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
         } else {
             tile32_load(acc, Aik, A.ld, wr, wc, lane);
         }
+        DF_STAMP(2);
         if (i == k) {  // diagonal tile: factor and publish (row i is then done)
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi)
@@ -471,11 +493,13 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
                         sm.d.T[(32 * wr + 16 * bi + F32_CROW(lane, r)) * DP + 32 * wc + 16 * bj +
                                (lane & 15)] = acc[bi][bj][r];
             __syncthreads();
+            DF_STAMP(5);
             if (wv == 0) {
                 const bool ok = diag_compute<true, float>(sm.d, lane);
                 if (lane == 0) sm.d.ok = ok;
             }
             __syncthreads();
+            DF_STAMP(6);
             if (!sm.d.ok) {
                 leave_failed();
                 return;
@@ -484,6 +508,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
                                            fd.Dinv + b * fd.dstride + (int64_t)i * 4096,
                                            fd.ldet + b * fd.lstride + i, threadIdx.x, 256);
             publish(base + c + 1);
+            DF_STAMP(7);
             return;
         }
         // panel TRSM: A_ik inv(L_kk)^T, the updated tile and inv(L_kk) staged as k_chol_panel32's
@@ -501,6 +526,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
             leave_failed();
             return;
         }
+        DF_STAMP(3);
         {
             const float* D = fd.Dinv + b * fd.dstride + (int64_t)k * 4096;
 #pragma unroll
@@ -538,6 +564,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
         if (pub) {
             tile32_store_sc1(x, Aik, A.ld, wr, wc, lane);
             publish(base + c + 1);
+            DF_STAMP(4);
         } else {
             tile32_store(x, Aik, A.ld, wr, wc, lane);
             __syncthreads();  // the staging area is reused by the next column's update

@@ -8,6 +8,6 @@ for v in "$@"; do
   rm -rf gpurun_out/ph_$v
   env $VAR=$v timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ph_$v -o run -- python3 tools/time_theta.py --batch 64 --reps 2 > gpurun_out/ph_$v.txt 2>&1
   T=$(find gpurun_out/ph_$v -name '*kernel_trace.csv' | head -1)
-  echo "== $VAR=$v"; grep "^hash" gpurun_out/ph_$v.txt; python3 tools/theta_phases.py $T
+  echo "== $VAR=$v"; grep "^hash\|^newton iter" gpurun_out/ph_$v.txt; python3 tools/theta_phases.py $T
   find gpurun_out/ph_$v -name '*.csv' -delete
 done

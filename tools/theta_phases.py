@@ -42,6 +42,11 @@ def main(path):
     if other:
         print('stream2: first {0:.2f} ms, last end {1:.2f} ms, {2} kernels'.format(
             (other[0][0] - t0) / 1e6, (max(r[1] for r in other) - t0) / 1e6, len(other)))
+    # Newton iterations: from one k_newton_prep to the next (the last ends at the last check)
+    preps = [r[0] for r in rows[:last_newton + 1] if r[2].startswith('k_newton_prep')]
+    ends = preps[1:] + [rows[last_newton][1]]
+    print('newton iterations (ms): ' + ' '.join('{0:.1f}'.format((e - a) / 1e6)
+                                                for a, e in zip(preps, ends)))
     top = collections.defaultdict(float)
     for s, e, n, q in rows[:end + 1]:
         top[(n, 'main' if q == main_q else 's2')] += (e - s) / 1e6

@@ -39,6 +39,7 @@ for r in range(a.reps):
     t2 = time.perf_counter()
     print('rep {0}: theta-call {1:.2f} ms  u-call {2:.3f} ms  logf {3}  status {4}  ops {5}'
           .format(r, 1e3 * (t1 - t0), 1e3 * (t2 - t1), out[:2], st[:2], nops[:2]), flush=True)
+print('newton iterations per chain (sorted):', sorted((np.asarray(nops) - 3).tolist()))
 print('hash theta-call {0} u-call {1}'.format(hashlib.sha1(out.tobytes()).hexdigest()[:16],
                                             hashlib.sha1(out2.tobytes()).hexdigest()[:16]))
 for k, name in ((0, 'gram'), (1, 'chol_update'), (2, 'ugemm'), (3, 'chol_update32'),
