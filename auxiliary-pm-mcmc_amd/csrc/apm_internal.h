@@ -196,6 +196,15 @@ void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t v
 // status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)
 void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s);
 
+// ---- newton.hip: read-back of up to three small device arrays (4-byte words) into mapped
+// pinned host memory, back to back at dst (device address of the host buffer)
+struct Export {
+    const unsigned* src[3];
+    int words[3];
+    unsigned* dst;
+};
+void launch_export(const Export& e, hipStream_t s);
+
 // ---- ugemm.hip ------------------------------------------------------------------------------
 struct UPool {
     float* base;        // each buffer: np x sp fp32, ld = sp, zero padded

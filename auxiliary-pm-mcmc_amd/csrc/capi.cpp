@@ -57,12 +57,16 @@ struct apm_ctx {
     double* refine_prev = nullptr;  // max|d| of the previous refinement step per chain
     int64_t n_refine_steps = 0, n_fp64_rerun = 0;  // statistics (apm_prof_read APM_PROF_STATS)
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;  // d_ubufs = d_slots + B
-    // pinned host staging of the per-call transfers (one H2D of slots + ubufs, D2H copies that
-    // are enqueued together and waited on once): [B slots][B ubufs][B out][B status][B n_iter]
-    // [B h3ok]
+    // pinned host staging of the per-call uploads (one H2D of slots + ubufs; the per-chain
+    // fp16x3 flags): [B slots][B ubufs][B h3ok]
     char* hpin = nullptr;
     int64_t* hblk = nullptr;  // pinned mirror of the d_i3 .. d_ctrs block (apm_u_normal/combine)
     double* hth = nullptr;    // pinned theta staging (B x P)
+    // read-back buffer: mapped, coherent pinned host memory (4B words) written by k_export
+    // (APM_EXPORT=0: filled by hipMemcpyAsync instead), dx its device address
+    unsigned* hx = nullptr;
+    unsigned* dx = nullptr;
+    bool export_rb = true;
     double *d_ca = nullptr, *d_cb = nullptr;
     uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
     double* U64 = nullptr;
@@ -430,6 +434,41 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
 
 void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
 
+// Read back up to three small per-chain device arrays (after the work enqueued so far on the
+// main stream) and wait: one k_export launch into the mapped host buffer (or one
+// hipMemcpyAsync per array with APM_EXPORT=0), a stream synchronisation, host copies.
+struct RB {
+    const void* src;
+    int bytes;
+    void* host;
+};
+void read_back(apm_ctx* c, std::initializer_list<RB> l) {
+    Export e{};
+    int k = 0, off = 0;
+    for (const RB& r : l) {
+        if (c->export_rb) {
+            e.src[k] = static_cast<const unsigned*>(r.src);
+            e.words[k] = r.bytes / 4;
+        } else {
+            HIPC(hipMemcpyAsync(reinterpret_cast<char*>(c->hx) + off, r.src, r.bytes,
+                                hipMemcpyDeviceToHost, c->stream));
+        }
+        off += r.bytes;
+        ++k;
+    }
+    if (c->export_rb) {
+        e.dst = c->dx;
+        launch_export(e, c->stream);
+        check_launch();
+    }
+    sync(c);
+    off = 0;
+    for (const RB& r : l) {
+        std::memcpy(r.host, reinterpret_cast<const char*>(c->hx) + off, r.bytes);
+        off += r.bytes;
+    }
+}
+
 // slots / ubufs of a call -> device in one copy from pinned memory
 void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubufs) {
     int64_t* h = reinterpret_cast<int64_t*>(c->hpin);
@@ -443,10 +482,7 @@ void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubuf
         HIPC(hipMemcpyAsync(c->d_slots, h, sizeof(int64_t) * count, hipMemcpyHostToDevice,
                             c->stream));
 }
-double* pin_out(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 16 * c->max_batch); }
-int* pin_status(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 32 * c->max_batch); }
-int* pin_iter(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 36 * c->max_batch); }
-int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 40 * c->max_batch); }
+int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 16 * c->max_batch); }
 
 // per-chain fp16x3 flags of a theta-call -> device (chol32.hip: |L_ij| <= sqrt(1 + K_ii) must
 // stay below fp16's range); h3_now = any chain flagged (else the fp32-operand kernel launches)
@@ -547,10 +583,7 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         ++c->n_refine_steps;
         if (last) break;
-        HIPC(hipMemcpyAsync(pin_iter(c), c->refining, sizeof(int) * count,
-                            hipMemcpyDeviceToHost, s));
-        sync(c);
-        std::memcpy(ref_h.data(), pin_iter(c), sizeof(int) * count);
+        read_back(c, {RB{c->refining, (int)sizeof(int) * count, ref_h.data()}});
         bool any = false;
         for (int b = 0; b < count; ++b) any |= ref_h[b] != 0;
         if (!any) break;
@@ -605,13 +638,8 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         launch_newton_check(c->v, c->n, c->np, c->tol, c->active, c->status, c->n_iter, count,
                             c->stream);
         check_launch();
-        HIPC(hipMemcpyAsync(pin_iter(c), c->active, sizeof(int) * count, hipMemcpyDeviceToHost,
-                            c->stream));
-        HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count,
-                            hipMemcpyDeviceToHost, c->stream));
-        sync(c);
-        std::memcpy(act.data(), pin_iter(c), sizeof(int) * count);
-        std::memcpy(st_h.data(), pin_status(c), sizeof(int) * count);
+        read_back(c, {RB{c->active, (int)sizeof(int) * count, act.data()},
+                      RB{c->status, (int)sizeof(int) * count, st_h.data()}});
         int live = 0;
         for (int b = 0; b < count; ++b) live += (act[b] != 0 && st_h[b] == 0);
         if (!live) break;
@@ -836,16 +864,9 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             u_eval_device(c, count);
         }
     }
-    HIPC(hipMemcpyAsync(pin_out(c), c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
-                        c->stream));
-    HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count, hipMemcpyDeviceToHost,
-                        c->stream));
-    HIPC(hipMemcpyAsync(pin_iter(c), c->n_iter, sizeof(int) * count, hipMemcpyDeviceToHost,
-                        c->stream));
-    sync(c);
-    std::memcpy(out_logf, pin_out(c), sizeof(double) * count);
-    std::memcpy(st_h.data(), pin_status(c), sizeof(int) * count);
-    std::memcpy(it_h.data(), pin_iter(c), sizeof(int) * count);
+    read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
+                  RB{c->status, (int)sizeof(int) * count, st_h.data()},
+                  RB{c->n_iter, (int)sizeof(int) * count, it_h.data()}});
     for (int b = 0; b < count; ++b) {
         status[b] = st_h[b];
         if (nops) {
@@ -885,6 +906,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_FUSE_DIAG")) c->fuse_diag = atoi(e) != 0;
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
+    if (const char* e = getenv("APM_EXPORT")) c->export_rb = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
@@ -956,7 +978,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 44, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 20, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 16,
+                       hipHostMallocMapped | hipHostMallocCoherent));
+    HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, B);
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1));
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * B * (c->nb + 1)));
@@ -988,6 +1013,7 @@ void free_ctx(apm_ctx* c) {
     if (c->hpin) (void)hipHostFree(c->hpin);
     if (c->hblk) (void)hipHostFree(c->hblk);
     if (c->hth) (void)hipHostFree(c->hth);
+    if (c->hx) (void)hipHostFree(c->hx);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1212,13 +1238,8 @@ int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* u
         upload_idx(c, (int)count, slots, ubufs);
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
         u_eval_device(c, (int)count);
-        HIPC(hipMemcpyAsync(pin_out(c), c->out, sizeof(double) * count, hipMemcpyDeviceToHost,
-                            c->stream));
-        HIPC(hipMemcpyAsync(pin_status(c), c->status, sizeof(int) * count,
-                            hipMemcpyDeviceToHost, c->stream));
-        sync(c);
-        std::memcpy(out_logf, pin_out(c), sizeof(double) * count);
-        std::memcpy(status, pin_status(c), sizeof(int) * count);
+        read_back(c, {RB{c->out, (int)sizeof(double) * (int)count, out_logf},
+                      RB{c->status, (int)sizeof(int) * (int)count, status}});
     } catch (const HipError& e) {
         return fail(c, APM_E_HIP, e.msg);
     }

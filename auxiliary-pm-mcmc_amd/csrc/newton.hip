@@ -339,3 +339,25 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
     hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
 }
+
+// Per-call read-back of small per-chain arrays (Newton flags, refinement mask, estimates,
+// status, iteration counts): one launch writes up to three device arrays straight into mapped,
+// coherent pinned host memory, replacing one hipMemcpyAsync each (every small D2H copy left the
+// GPU idle ~77 us before its blit, profiles/r02_idle_gaps.txt). The host reads after the
+// stream synchronisation that follows.
+__global__ __launch_bounds__(256) void k_export(Export e) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    int off = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (t >= off && t < off + e.words[k]) e.dst[t] = e.src[k][t - off];
+        off += e.words[k];
+    }
+    __threadfence_system();
+}
+
+void launch_export(const Export& e, hipStream_t s) {
+    const int tot = e.words[0] + e.words[1] + e.words[2];
+    if (tot <= 0) return;
+    hipLaunchKernelGGL(k_export, dim3((tot + 255) / 256), dim3(256), 0, s, e);
+}

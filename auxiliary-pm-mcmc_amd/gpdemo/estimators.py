@@ -28,16 +28,21 @@ class InvalidCovarianceMatrixError(Exception):
 
 class DeviceCache(object):
     """Handle to the per-theta state kept on the device (replaces the reference's
-    ``(K_chol, C_chol, f_post)`` tuple / ``K_chol`` array). Iterating it reads the state back
-    as ``(None, factor, f_post)`` (IS: factor = C_chol; K_chol is never formed on the device,
-    DESIGN.md §3) for inspection; the samplers only pass it back."""
+    ``(K_chol, C_chol, f_post)`` tuple / ``K_chol`` array). Iterating an IS cache reads the
+    state back as that tuple (reference estimators.py:166-176) for inspection; the samplers only
+    pass the handle back. The slot keeps C_chol and f_post; L_K = chol(K) is consumed by the
+    posterior factor on the device, so iterating refactors K on the device
+    (a PriorMC theta-call into a scratch slot) — all three factors are read back rounded to fp32
+    like the slot itself."""
 
-    __slots__ = ('_ctx', 'slot', 'kind', '__weakref__')
+    __slots__ = ('_ctx', 'slot', 'kind', '_owner', '_theta', '__weakref__')
 
-    def __init__(self, ctx, slot, kind):
+    def __init__(self, ctx, slot, kind, owner=None, theta=None):
         self._ctx = ctx
         self.slot = slot
         self.kind = kind
+        self._owner = owner  # the estimator (its kernel_func / X) for the K_chol refactor
+        self._theta = None if theta is None else np.array(theta, dtype=np.float64)
 
     def __del__(self):
         try:
@@ -49,9 +54,30 @@ class DeviceCache(object):
         """(factor (n, n) lower, f_post (n,), g (n,), const) — factor rounded to fp32."""
         return self._ctx.slot_read(self.slot)
 
+    def k_chol(self):
+        """chol(K(theta)) (n, n) lower, computed on the device (fp32-rounded read-back)."""
+        if self.kind == _native.EST_PRIORMC:
+            return self.read()[0]
+        if self._owner is None or self._theta is None:
+            raise ValueError('this cache does not record its theta')
+        tmp = self._ctx.slots.acquire()
+        try:
+            _, st, _ = self._owner._theta_call(_native.EST_PRIORMC, self._ctx, self._theta,
+                                               _UBUF, tmp)
+            _raise_for_status(int(st[0]), self._ctx)
+            return self._ctx.slot_read(tmp)[0]
+        finally:
+            self._ctx.slots.release(tmp)
+
     def __iter__(self):
         L, f, _, _ = self.read()
-        return iter((None, L, f))
+        if self.kind == _native.EST_PRIORMC:  # the reference's K_chol is the array itself
+            return iter(L)
+        return iter((self.k_chol(), L, f))
+
+    def __array__(self, dtype=None, copy=None):
+        L = self.read()[0] if self.kind == _native.EST_PRIORMC else self.k_chol()
+        return L if dtype is None else L.astype(dtype)
 
 
 def _kernel_spec(kernel_func):
@@ -154,7 +180,7 @@ class LogMarginalLikelihoodApproxPosteriorISEstimator(_EstimatorBase):
             ctx = self._prob.ctx(ns.shape[1])
             ctx.u_upload(_UBUF, ns)
             slot = ctx.slots.acquire()
-            cache = DeviceCache(ctx, slot, _native.EST_IS)
+            cache = DeviceCache(ctx, slot, _native.EST_IS, self, theta)
             out, st, nops = self._theta_call(_native.EST_IS, ctx, theta, _UBUF, slot)
             _raise_for_status(int(st[0]), ctx)
             self.n_cubic_ops += int(nops[0])
@@ -182,7 +208,7 @@ class LogMarginalLikelihoodPriorMCEstimator(_EstimatorBase):
             ctx = self._prob.ctx(ns.shape[1])
             ctx.u_upload(_UBUF, ns)
             slot = ctx.slots.acquire()
-            cache = DeviceCache(ctx, slot, _native.EST_PRIORMC)
+            cache = DeviceCache(ctx, slot, _native.EST_PRIORMC, self, theta)
             out, st, nops = self._theta_call(_native.EST_PRIORMC, ctx, theta, _UBUF, slot)
             _raise_for_status(int(st[0]), ctx)
             self.n_cubic_ops += int(nops[0])

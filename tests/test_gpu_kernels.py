@@ -109,6 +109,34 @@ def test_is_estimator_vs_golden(nat):
         ctx.close()
 
 
+def test_cache_tuple_vs_golden(nat):
+    """Iterating the API's IS cache yields the reference's (K_chol, C_chol, f_post) tuple
+    (estimators.py:166-176); a PriorMC cache converts to the reference's K_chol array
+    (estimators.py:311-318). fp32-rounded read-back."""
+    import gpdemo.estimators as est
+    import gpdemo.kernels as krn
+    import gpdemo.latent_posterior_approximations as lpa
+    for ci, c in enumerate(_cases()):
+        kf = krn.make_kernel_func(str(c['kind']), 1e-8)
+        e = est.LogMarginalLikelihoodApproxPosteriorISEstimator(c['X'], c['y'], kf,
+                                                                lpa.laplace_approximation)
+        _, cache = e(c['ns1'], c['theta'])
+        ops = e.n_cubic_ops
+        K_chol, C_chol, f_post = cache
+        assert e.n_cubic_ops == ops  # inspection is not an estimator op
+        for got, ref in ((K_chol, c['K_chol']), (C_chol, c['C_chol'])):
+            np.testing.assert_allclose(got, np.tril(ref), rtol=0,
+                                       atol=2e-6 * np.abs(ref).max(), err_msg=str(ci))
+        np.testing.assert_allclose(f_post, c['f_post'], rtol=1e-8, atol=1e-10)
+        # the cache still serves u-calls after the inspection's scratch theta-call
+        v2, _ = e(c['ns2'], None, cache)
+        assert _close(v2, float(c['is_logf2'])), (ci, v2)
+        p = est.LogMarginalLikelihoodPriorMCEstimator(c['X'], c['y'], kf)
+        _, kc = p(c['ns1'], c['theta'])
+        np.testing.assert_allclose(np.asarray(kc), np.tril(c['K_chol']), rtol=0,
+                                   atol=2e-6 * np.abs(c['K_chol']).max(), err_msg=str(ci))
+
+
 def test_priormc_and_laplace_estimators_vs_golden(nat):
     for ci, c in enumerate(_cases()):
         ctx = _ctx(nat, c)
