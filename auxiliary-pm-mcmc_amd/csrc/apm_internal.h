@@ -87,12 +87,17 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
                           int hlim = 0, const int* h3ok = nullptr);
 // the same update with one 128x128 super-tile per workgroup (tiles from build_update_supertiles);
 // hlim > 0: fp16x3 operands (chol32.hip) for super-tiles whose rows lie below row tile hlim, in
-// the chains b with h3ok[b] != 0 (h3ok == nullptr: every chain); the others take fp32 operands
+// the chains b with h3ok[b] != 0 (h3ok == nullptr: every chain); the others take fp32 operands.
+// rhs >= 0: row tile rhs is the appended right-hand side whose first row alone is data (its
+// super-tiles must hold it alone: build_update_supertiles(..., solo = rhs)); it is updated as a
+// row-vector product (fp64 accumulation) instead of a 64-row tile product
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
-                               int hlim = 0, const int* h3ok = nullptr);
-std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi);
+                               int hlim = 0, const int* h3ok = nullptr, int rhs = -1);
+// solo >= 0: row tile solo gets super-tile rows of its own (never paired with another row tile)
+std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
+                                              int solo = -1);
 // y = K x from K's lower tiles (part: nb*nb*64 doubles per chain of partials); Bf.base != null
 // also forms the fp32 Newton matrix I + W^1/2 K W^1/2 and its right-hand-side block (x = b)
 void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,

@@ -85,6 +85,8 @@ struct apm_ctx {
     // update-tile lists per launch shape (i0, R, j0, jend), built once, kept on the device
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
+    std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
+    bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     int t128 = 3;
     bool left_inner = true;
@@ -245,7 +247,8 @@ std::pair<unsigned*, int> tile_list(apm_ctx* c, int i0, int R, int j0, int jend,
 // Trailing update of tiles (i, j), i in [i0, R) minus the gap, j in [j0, min(i, jend-1)], by
 // columns [k0, k0+kc). fuse_k >= 0: the launch also factors diagonal tile (fuse_k, fuse_k), which
 // must be its first tile (i0 == j0 == fuse_k; the super-tile order starts there).
-std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g);
+std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g,
+                                     int solo = -1);
 
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
                     int plus, int count, int fuse_k = -1, int fail_code = 0,
@@ -335,15 +338,17 @@ MatF b32_of(apm_ctx* c) {
 }
 float* dinv32_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv); }
 
-std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g) {
+std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend, Gap g,
+                                     int solo) {
+    auto& lists = solo >= 0 ? c->super_lists_solo : c->super_lists;
     auto key = std::make_tuple(i0, R, j0, jend, g.lo, g.hi);
-    auto it = c->super_lists.find(key);
-    if (it != c->super_lists.end()) return it->second;
-    std::vector<unsigned> v = build_update_supertiles(i0, R, j0, jend, g.lo, g.hi);
+    auto it = lists.find(key);
+    if (it != lists.end()) return it->second;
+    std::vector<unsigned> v = build_update_supertiles(i0, R, j0, jend, g.lo, g.hi, solo);
     unsigned* d = dalloc<unsigned>(c, v.size());
     HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
     auto val = std::make_pair(d, (int)v.size());
-    c->super_lists[key] = val;
+    lists[key] = val;
     return val;
 }
 
@@ -360,9 +365,12 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl);
     if ((c->t128 & 1) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
-        const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0});
+        // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a
+        // row vector (APM_RHS_ROW=0: as a 64-row tile)
+        const int rhs = c->rhs_row && R > c->nb ? c->nb : -1;
+        const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  fd, c->h3_now ? c->nb : 0, c->h3ok);
+                                  fd, c->h3_now ? c->nb : 0, c->h3ok, rhs);
     } else {
         launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd,
                              c->h3_now ? c->nb : 0, c->h3ok);
@@ -907,6 +915,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
     if (const char* e = getenv("APM_EXPORT")) c->export_rb = atoi(e) != 0;
+    if (const char* e = getenv("APM_RHS_ROW")) c->rhs_row = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;

@@ -619,12 +619,62 @@ struct __attribute__((aligned(16))) GemmSmemH3 {
 #ifndef H3_ABL
 #define H3_ABL 0
 #endif
+
+// Update of the appended right-hand-side row tile of the Newton matrix, whose first row alone
+// holds data (k_symv_reduce zeroes the other 63): C[0][c] -= sum_k A[0][k] B[c][k] for the 64 or
+// 128 columns c of the super-tile, as row-vector products instead of a 64-row MFMA tile (which
+// also had to take fp32 operands: the row is not bounded like the entries of L). Wave w takes 32
+// of the 128 columns, 4 at a time; lane l multiplies k = 4l + 256q .. +3 (16-byte loads, each
+// B row read as one contiguous 64-lane access), fp64 accumulation, butterfly reduction - a fixed
+// order, so the result does not depend on the schedule.
+__device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, int tj, bool cv0,
+                                                 bool cv1, int k0, int kc, int tid) {
+    const int lane = tid & 63, w = tid >> 6;
+    if (!(w < 2 ? cv0 : cv1)) return;
+    const int K = 64 * kc;  // <= 64 * 14
+    constexpr int QM = 4;
+    float* crow = Ab + (int64_t)(ti * 64) * ld;
+    const float* arow = crow + k0 * 64;
+    f4_t a[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q)
+        a[q] = (4 * lane + 256 * q < K) ? *reinterpret_cast<const f4_t*>(arow + 4 * lane + 256 * q)
+                                        : f4_t{0.f, 0.f, 0.f, 0.f};
+    const int c0 = (w < 2 ? tj * 64 : (tj + 1) * 64) + 32 * (w & 1);
+#pragma unroll 1
+    for (int r0 = 0; r0 < 32; r0 += 4) {
+        f4_t v[4][QM];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const float* brow = Ab + (int64_t)(c0 + r0 + rr) * ld + k0 * 64 + 4 * lane;
+#pragma unroll
+            for (int q = 0; q < QM; ++q)
+                v[rr][q] = (4 * lane + 256 * q < K) ? *reinterpret_cast<const f4_t*>(brow + 256 * q)
+                                                    : f4_t{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < QM; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s = fma((double)a[q][e], (double)v[rr][q][e], s);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+            if (lane == rr) {
+                float* cp = crow + c0 + r0 + rr;
+                *cp = (float)((double)*cp - s);
+            }
+        }
+    }
+}
 template <bool H3>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
                                                                FusedDiag<float> fd, int hlim,
-                                                               const int* __restrict__ h3ok) {
+                                                               const int* __restrict__ h3ok,
+                                                               int rhs) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     __shared__ union {
@@ -652,6 +702,10 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
     const int ra0 = rv0 ? ti : ti + 1, ra1 = rv1 ? ti + 1 : ti;
     const int cb0 = cv0 ? tj : tj + 1, cb1 = cv1 ? tj + 1 : tj;
     float* Ab = A.base + b * A.cstride;
+    if (ti == rhs) {  // the right-hand-side row alone (its super-tile row holds no other tile)
+        rhs_row_update32(Ab, A.ld, ti, tj, cv0, cv1, k0, kc, tid);
+        return;
+    }
     // this wave's output tile
     const int oi = ti + wr, oj = tj + wc;
     const bool mine = (wr ? rv1 : rv0) && (wc ? cv1 : cv0) && oj <= oi;
@@ -668,7 +722,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
             for (int r = 0; r < 4; ++r)
                 acc[bi][bj][r] = -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
     // super-tile rows below hlim (the appended right-hand side row), chains flagged in h3ok
-    if (H3 && ti + 1 < hlim && (!h3ok || h3ok[b])) {
+    if (H3 && ti + (rv1 ? 1 : 0) < hlim && (!h3ok || h3ok[b])) {
         // register staging: thread tid moves 16-byte pieces p = tid + 256h (row p/8, k 4(p%8))
         // of both operands
         const float* arow[4];
@@ -751,7 +805,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         __syncthreads();
         for (int s = 0; s < nsub; ++s) {
             if (s + 1 < nsub) gload(s + 1, ra, rb);
-            compute(s & 1);
+            if (mine) compute(s & 1);  // a wave whose tile is dropped only stages
             if (s + 1 < nsub) sstore((s + 1) & 1, ra, rb);
             __syncthreads();
         }
@@ -810,7 +864,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         __syncthreads();
         for (int s = 0; s < nsub; ++s) {
             if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
-            compute(s & 1);
+            if (mine) compute(s & 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
@@ -860,31 +914,40 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
-                               int hlim, const int* h3ok) {
+                               int hlim, const int* h3ok, int rhs) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     if (hlim > 0)
         hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok);
+                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs);
     else
         hipLaunchKernelGGL(k_chol_update32_t128<false>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr);
+                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr, rhs);
 }
 
 // Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),
 // j0 <= j <= min(i, jend-1), in 4x4-super-tile blocks (the L2 locality of build_update_tiles);
 // super-tile rows start at i0, columns at j0. Entries without any valid tile are omitted.
-std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi) {
+std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
+                                              int solo) {
     std::vector<unsigned> v;
     auto rowv = [&](int i) { return i < R && !(i >= glo && i < ghi); };
     const int S = 4;  // super-tiles per block edge (8x8 tiles, as build_update_tiles)
-    const int nr = (R - i0 + 1) / 2, nc = (jend - j0 + 1) / 2;
+    std::vector<int> rows;  // first row tile of each super-tile row; rows[p] + 1 valid iff paired
+    std::vector<bool> pair;
+    for (int i = i0; i < R;) {
+        const bool two = i != solo && i + 1 != solo;
+        rows.push_back(i);
+        pair.push_back(two);
+        i += two ? 2 : 1;
+    }
+    const int nr = (int)rows.size(), nc = (jend - j0 + 1) / 2;
     for (int P = 0; P < nr; P += S)
         for (int Q = 0; Q < nc; Q += S)
             for (int p = P; p < std::min(P + S, nr); ++p)
                 for (int q = Q; q < std::min(Q + S, nc); ++q) {
-                    const int i = i0 + 2 * p, j = j0 + 2 * q;
-                    const bool rv0 = rowv(i), rv1 = rowv(i + 1);
+                    const int i = rows[p], j = j0 + 2 * q;
+                    const bool rv0 = rowv(i), rv1 = pair[p] && rowv(i + 1);
                     const bool cv0 = j < jend, cv1 = j + 1 < jend;
                     bool any = false;
                     for (int a = 0; a < 2; ++a)
