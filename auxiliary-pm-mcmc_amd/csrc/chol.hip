@@ -474,7 +474,10 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
     __syncthreads();
     for (int s = 0; s < nsub; ++s) {
         if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
-        compute(s & 1);
+        // a wave whose tile is dropped (diagonal super-tile's upper half, invalid half) only
+        // stages; in the SYRK a wave's tile column oj needs Y's column blocks k <= oj only (the
+        // rest of the workgroup's depth multiplies zeros)
+        if (mine && (!INIT || (s * KS64T) / 64 <= oj)) compute(s & 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
