@@ -135,10 +135,10 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 // ---- gram.hip -------------------------------------------------------------------------------
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
 // kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
-// both: write both triangles (else K's lower tiles only)
+// both: write both triangles (else K's lower tiles only); K2.base: the lower tiles also to K2
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both);
+                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0});
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)

@@ -87,6 +87,7 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
+    bool gram2 = true;    // APM_GRAM2=0: K's working copies by k_copy_lower instead of the Gram
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     int t128 = 3;
     bool left_inner = true;
@@ -725,11 +726,13 @@ void chol_k_panel(apm_ctx* c, const Exec& ex) {
                c->cholk_count, true, 0, no_gap, &ex);
     c->cholk_next = K + OUTER;
 }
-void chol_k_begin(apm_ctx* c, int count, const Exec& ex) {
+void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true) {
     HIPC(hipMemsetD32Async(c->active2, 1, count, ex.s));
     HIPC(hipMemsetAsync(c->status2, 0, sizeof(int) * count, ex.s));
-    launch_copy_lower(c->K, bl_of(c), c->np, ex.lv, count, ex.s);
-    check_launch();
+    if (copy) {  // (else the Gram wrote K's lower tiles into BL as well)
+        launch_copy_lower(c->K, bl_of(c), c->np, ex.lv, count, ex.s);
+        check_launch();
+    }
     c->cholk_next = 0;
     c->cholk_count = count;
     chol_k_panel(c, ex);
@@ -813,6 +816,15 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
     HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
+    // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
+    const bool ov = est == APM_EST_IS && !c->postcov_aug && c->mixed && c->overlap_k;
+    // the matrix a factorisation of K starts from (chol(K)'s working copy BL, or PriorMC's A):
+    // the Gram writes K's lower tiles there too instead of a later copy pass (APM_GRAM2=0: copy)
+    MatB k2{nullptr, 0, 0};
+    if (gram && c->gram2 && !c->postcov_aug) {
+        if (est == APM_EST_PRIORMC) k2 = c->A;
+        else if (ov) k2 = bl_of(c);
+    }
     if (gram) {
         // the augmented posterior route (APM_POSTCOV=aug) reads K's upper tiles; every other
         // consumer reads the lower ones: the Gram then writes N(N+1)/2 entries
@@ -820,25 +832,25 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         const double nk = c->k_full ? (double)c->n * c->n : 0.5 * (double)c->n * (c->n + 1);
         ProfScope ps(c, APM_PROF_GRAM, 8.0 * ((double)c->n * c->d + nk) * count + 8.0 * c->P);
         launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
-                    count, c->stream, c->k_full);
+                    count, c->stream, c->k_full, k2);
         check_launch();
     }
     std::vector<int> st_h(count, 0), it_h(count, 0);
     if (est == APM_EST_PRIORMC) {
-        launch_copy_lower(c->K, c->A, c->np, lv, count, c->stream);
-        check_launch();
+        if (!k2.base) {
+            launch_copy_lower(c->K, c->A, c->np, lv, count, c->stream);
+            check_launch();
+        }
         chol_range(c, c->A, 0, c->nb, c->nb, c->nb, APM_STATUS_CHOL_K, count);
         launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 1, c->n,
                           c->np, lv, count, c->stream);
         check_launch();
         u_eval_device(c, count);
     } else {
-        // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
-        const bool ov = est == APM_EST_IS && !c->postcov_aug && c->mixed && c->overlap_k;
         if (ov) {
             HIPC(hipEventRecord(c->ev_gram, c->stream));
             HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
-            chol_k_begin(c, count, k_exec(c, c->stream2));
+            chol_k_begin(c, count, k_exec(c, c->stream2), /*copy=*/k2.base == nullptr);
         }
         const int64_t reruns = c->n_fp64_rerun;
         if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself
@@ -916,6 +928,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
     if (const char* e = getenv("APM_EXPORT")) c->export_rb = atoi(e) != 0;
     if (const char* e = getenv("APM_RHS_ROW")) c->rhs_row = atoi(e) != 0;
+    if (const char* e = getenv("APM_GRAM2")) c->gram2 = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;

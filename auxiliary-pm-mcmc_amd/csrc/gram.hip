@@ -19,7 +19,7 @@
 __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__ X, int64_t ldx,
                                               int n, int d, const double* __restrict__ theta,
                                               int64_t tstride, int kind, double eps, Live live,
-                                              int both) {
+                                              int both, MatB K2) {
     const int b = blockIdx.y;
     if (live.active[b] == 0 || live.status[b] != 0) return;
     // lower-triangular tile index -> (ti, tj), ti >= tj
@@ -95,6 +95,15 @@ __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__
         *reinterpret_cast<d2_t*>(dst + 2 * tc) = d2_t{v[p][0], v[p][1]};
         *reinterpret_cast<d2_t*>(dst + 32 + 2 * tc) = d2_t{v[p][2], v[p][3]};
     }
+    if (K2.base) {  // second copy of the lower tiles (the concurrent chol(K)'s working copy)
+        double* K2b = K2.base + b * K2.cstride;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            double* dst = K2b + (int64_t)(ti * 64 + RO(tr, p)) * K2.ld + tj * 64;
+            *reinterpret_cast<d2_t*>(dst + 2 * tc) = d2_t{v[p][0], v[p][1]};
+            *reinterpret_cast<d2_t*>(dst + 32 + 2 * tc) = d2_t{v[p][2], v[p][3]};
+        }
+    }
     if (both && ti != tj) {  // transposed tile (tj, ti)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -107,8 +116,8 @@ __global__ __launch_bounds__(256) void k_gram(MatB K, const double* __restrict__
 
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both) {
+                 hipStream_t s, bool both, MatB K2) {
     const int nb = np / 64;
     hipLaunchKernelGGL(k_gram, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx, n,
-                       d, theta, tstride, kind, eps, live, (int)both);
+                       d, theta, tstride, kind, eps, live, (int)both, K2);
 }
