@@ -381,13 +381,14 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
         return False
 
     def run_async(self, n_steps, keep_going=False):
-        """Advance every live chain by at least ``n_steps`` transitions with the asynchronous
-        schedule. keep_going=False: a chain stops after n_steps (the call ends with every chain
-        at a transition boundary); True: chains that are ahead keep working until the slowest
+        """Advance every live chain by at least ``n_steps`` transitions (a number, or one per
+        chain) with the asynchronous schedule. keep_going=False: a chain stops after n_steps
+        (the call ends with every chain at a transition boundary); True: chains that are ahead keep working until the slowest
         has n_steps (throughput mode; a final partial transition is discarded).
         Returns (traces, done): per chain the list of thetas after each completed transition and
         the number of completed transitions."""
         C = self.n_chains
+        n_steps = np.broadcast_to(np.asarray(n_steps, dtype=np.int64), (C,))  # or per chain
         done = np.zeros(C, dtype=np.int64)
         traces = [[] for _ in range(C)]
         need_u = ~self.failed

@@ -80,7 +80,8 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
 // base per factorisation and panel)
 void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, hipStream_t s);
+                            int64_t pstride, unsigned long long base,
+                            unsigned long long* timeouts, hipStream_t s);
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},

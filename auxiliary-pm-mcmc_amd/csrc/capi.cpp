@@ -36,6 +36,7 @@ struct apm_ctx {
     bool fuse_diag = true;  // APM_FUSE_DIAG=0: stand-alone diag launches (development knob)
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
+    std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
     double eps = 1e-8, tol = 1e-4;
     int64_t max_iters = 1000;
     std::string err;
@@ -385,7 +386,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
-    const bool df = c->df32 && c->fuse_diag && c->left_inner && OUTER32 <= 14;
+    const bool df = c->df32 && c->fuse_diag && c->left_inner;
     const unsigned long long fact = ++c->df_fact;
     for (int K = k0; K < k1; K += OUTER32) {
         const int Kend = std::min(K + OUTER32, k1);
@@ -395,11 +396,12 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
+            if (Kend - K > 14) throw HipError{"dataflow Newton panel wider than 14 tiles"};
             launch_chol_panel_df32(M, K, Kend - K, R,
                                    FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
                                    count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
                                    (fact << 16) | ((unsigned long long)(K / OUTER32) << 4),
-                                   c->stream);
+                                   c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream);
             check_launch();
             have_diag = Kend < k1;
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
@@ -911,7 +913,9 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
     if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
-    if (const char* e = getenv("APM_OUTER32")) OUTER32 = std::max(1, atoi(e));
+    // the Newton panels: <= 14 tiles (the dataflow panel's progress word packs the column step in
+    // 4 bits, 15 = failed; rhs_row_update32 covers a depth of 16 tiles)
+    if (const char* e = getenv("APM_OUTER32")) OUTER32 = std::min(14, std::max(1, atoi(e)));
     if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
     if (const char* e = getenv("APM_SCHED")) {  // host wait policy of synchronisations
         const std::string m(e);
@@ -956,6 +960,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->sp = (int)((S + 63) / 64 * 64);
     c->max_batch = (int)max_batch;
     c->n_slots = (int)n_slots;
+    c->slot_refs.assign((size_t)n_slots, 0);
     c->n_ubufs = (int)n_ubufs;
     c->eps = eps;
     const int64_t np = c->np, B = max_batch;
@@ -1005,8 +1010,9 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, B);
-    c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1));
-    HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * B * (c->nb + 1)));
+    // + 1: the count of bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS)
+    c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 1);
+    HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 1)));
     // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:
     // [i3: 3B int64][ca: B][cb: B][seeds: B][ctrs: B]
     c->d_i3 = dalloc<int64_t>(c, 7 * B);
@@ -1268,6 +1274,41 @@ int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* u
     return APM_SUCCESS;
 }
 
+// ---- cache-slot lifetimes (samplers.py:563-584: an MH sampler holds the current state's cache
+// and the proposal's at once; on accept the proposal's becomes current and the old one is dropped).
+// Host bookkeeping only: a slot's contents are immutable between theta-calls into it, so a copy
+// of the handle is another owner of the same state, as a second reference to the reference's
+// (K_chol, C_chol, f_post) tuple is.
+int apm_cache_acquire(apm_ctx* c, int64_t* slot) {
+    if (!c || !slot) return fail(c, APM_E_INVALID, "apm_cache_acquire: bad arguments");
+    for (int i = 0; i < c->n_slots; ++i)
+        if (c->slot_refs[i] == 0) {
+            c->slot_refs[i] = 1;
+            *slot = i;
+            return APM_SUCCESS;
+        }
+    return fail(c, APM_E_NOMEM, "apm_cache_acquire: every cache slot is owned (raise n_slots)");
+}
+
+int apm_cache_copy(apm_ctx* c, int64_t slot) {
+    if (!c || slot < 0 || slot >= c->n_slots || c->slot_refs[slot] <= 0)
+        return fail(c, APM_E_INVALID, "apm_cache_copy: slot not acquired");
+    ++c->slot_refs[slot];
+    return APM_SUCCESS;
+}
+
+int apm_cache_release(apm_ctx* c, int64_t slot) {
+    if (!c || slot < 0 || slot >= c->n_slots || c->slot_refs[slot] <= 0)
+        return fail(c, APM_E_INVALID, "apm_cache_release: slot not acquired");
+    --c->slot_refs[slot];
+    return APM_SUCCESS;
+}
+
+int64_t apm_cache_refcount(const apm_ctx* c, int64_t slot) {
+    if (!c || slot < 0 || slot >= c->n_slots) return APM_E_INVALID;
+    return c->slot_refs[slot];
+}
+
 int apm_slot_read(apm_ctx* c, int64_t slot, double* L, int64_t ldl, double* f_post, double* g,
                   double* cst) {
     if (!c || slot < 0 || slot >= c->n_slots) return fail(c, APM_E_INVALID, "apm_slot_read: bad slot");
@@ -1478,6 +1519,16 @@ int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, dou
     try {
         HIPC(hipSetDevice(c->device));
         sync(c);
+        if (kind == APM_PROF_DF_TIMEOUTS) {
+            unsigned long long* d = c->dfprog + (size_t)c->max_batch * (c->nb + 1);
+            unsigned long long h = 0;
+            HIPC(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost));
+            if (total_ms) *total_ms = 0.0;
+            if (launches) *launches = (int64_t)h;
+            if (work) *work = 0.0;
+            if (reset) HIPC(hipMemset(d, 0, sizeof(h)));
+            return APM_SUCCESS;
+        }
         if (kind == APM_PROF_STATS) {
             if (total_ms) *total_ms = 0.0;
             if (launches) *launches = c->n_fp64_rerun;

@@ -368,7 +368,8 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
                                                          const int* __restrict__ h3ok,
                                                          unsigned long long* prog,
                                                          int64_t pstride,
-                                                         unsigned long long base) {
+                                                         unsigned long long base,
+                                                         unsigned long long* timeouts) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -393,7 +394,8 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
             unsigned long long v =
                 __hip_atomic_load(pr + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int spins = 0; v < need; ++spins) {
-                if (spins > DF_SPIN) {
+                if (spins > DF_SPIN) {  // counted apart from breakdowns (APM_PROF_DF_TIMEOUTS)
+                    atomicAdd(timeouts, 1ull);
                     v = base + DF_FAILED;
                     break;
                 }
@@ -574,11 +576,13 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
 
 void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, hipStream_t s) {
-    if (ncols < 1 || ncols > 14 || R - K <= 1) return;  // (one column: its panel TRSM)
+                            int64_t pstride, unsigned long long base,
+                            unsigned long long* timeouts, hipStream_t s) {
+    // ncols <= 14 is the caller's contract (chol_range32 throws before launching wider panels)
+    if (ncols < 1 || R - K <= 1) return;  // (one column: its panel TRSM)
     const long total = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32, dim3((unsigned)total), dim3(256), 0, s, A, K, ncols,
-                       nchains, fd, live, hlim, h3ok, prog, pstride, base);
+                       nchains, fd, live, hlim, h3ok, prog, pstride, base, timeouts);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -631,7 +635,7 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
                                                  bool cv1, int k0, int kc, int tid) {
     const int lane = tid & 63, w = tid >> 6;
     if (!(w < 2 ? cv0 : cv1)) return;
-    const int K = 64 * kc;  // <= 64 * 14
+    const int K = 64 * kc;  // <= 64 * 14 (OUTER32 is clamped to 14 tiles: capi.cpp init_ctx)
     constexpr int QM = 4;
     float* crow = Ab + (int64_t)(ti * 64) * ld;
     const float* arow = crow + k0 * 64;

@@ -16,9 +16,10 @@ LIB_PATH = os.environ.get('APM_LIB', os.path.join(_PKG_ROOT, 'lib', 'libapm.so')
 # include/apm.h constants
 KERNEL_ISO, KERNEL_ARD, KERNEL_PRECOMPUTED = 0, 1, 2
 EST_IS, EST_PRIORMC, EST_LAPLACE = 0, 1, 2
+APM_SUCCESS, APM_E_INVALID, APM_E_HIP, APM_E_NOMEM = 0, -1, -2, -3
 STATUS_OK, STATUS_CHOL_K, STATUS_CHOL_B, STATUS_CHOL_C, STATUS_MAXITER = 0, 1, 2, 3, 4
 PROF_GRAM, PROF_CHOL_UPDATE, PROF_UGEMM, PROF_CHOL_UPDATE32, PROF_STATS = 0, 1, 2, 3, 4
-PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER, PROF_NKINDS = 5, 6, 7
+PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER, PROF_DF_TIMEOUTS, PROF_NKINDS = 5, 6, 7, 8
 
 
 class NativeUnavailableError(RuntimeError):
@@ -53,6 +54,10 @@ _SIGS = {
     'apm_theta_eval_K': (_i, [_p, _i, _p, _i64, _i64, _i64, _p, _p, _p]),
     'apm_u_eval': (_i, [_p, _i64, _p, _p, _p, _p]),
     'apm_slot_read': (_i, [_p, _i64, _p, _i64, _p, _p, _p]),
+    'apm_cache_acquire': (_i, [_p, _p]),
+    'apm_cache_copy': (_i, [_p, _i64]),
+    'apm_cache_release': (_i, [_p, _i64]),
+    'apm_cache_refcount': (_i64, [_p, _i64]),
     'apm_gram': (_i, [_i, _i, _p, _i64, _i64, _i64, _p, _i64, _d, _p, _i64]),
     'apm_laplace': (_i, [_i, _p, _i64, _i64, _p, _i, _i, _d, _i64, _p, _p, _i64, _p, _p, _p]),
     'apm_prof_enable': (_i, [_p, _i]),
@@ -192,6 +197,29 @@ class _Pool(object):
             self.free.append(i)
 
 
+class _SlotPool(object):
+    """Cache-slot owners kept by the library (apm_cache_acquire / _copy / _release): the same
+    interface as _Pool, so a C caller and this layer share one ownership record."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def acquire(self):
+        s = ctypes.c_int64(-1)
+        _check(self.ctx.lib.apm_cache_acquire(self.ctx._h, ctypes.byref(s)), self.ctx._h)
+        return int(s.value)
+
+    def incref(self, i):
+        _check(self.ctx.lib.apm_cache_copy(self.ctx._h, int(i)), self.ctx._h)
+
+    def release(self, i):
+        if self.ctx._h:
+            _check(self.ctx.lib.apm_cache_release(self.ctx._h, int(i)), self.ctx._h)
+
+    def refcount(self, i):
+        return int(self.ctx.lib.apm_cache_refcount(self.ctx._h, int(i)))
+
+
 class Context(object):
     """A device-resident problem (X, y, kernel) with workspaces for up to `max_batch` chains."""
 
@@ -217,7 +245,7 @@ class Context(object):
         if not self._h:
             raise NativeError('apm_create failed: ' +
                               (lib.apm_global_error() or b'').decode(errors='replace'))
-        self.slots = _Pool(int(n_slots))
+        self.slots = _SlotPool(self)
         self.ubufs = _Pool(int(n_ubufs))
         # calls per batch size (bench.py reports the timed region's; launch shapes depend on it)
         self.batch_hist = {'u': collections.Counter(), 'theta': collections.Counter()}

@@ -33,9 +33,11 @@ class DeviceCache(object):
     pass the handle back. The slot keeps C_chol and f_post; L_K = chol(K) is consumed by the
     posterior factor on the device, so iterating refactors K on the device
     (a PriorMC theta-call into a scratch slot) — all three factors are read back rounded to fp32
-    like the slot itself."""
+    like the slot itself. That refactor runs once per handle (memoised): an O(N^3) device call,
+    so unpacking the tuple is not free the first time. ``numpy.asarray`` is defined for a PriorMC
+    handle only (the reference's K_chol array); an IS handle is a tuple, not an array."""
 
-    __slots__ = ('_ctx', 'slot', 'kind', '_owner', '_theta', '__weakref__')
+    __slots__ = ('_ctx', 'slot', 'kind', '_owner', '_theta', '_kchol', '__weakref__')
 
     def __init__(self, ctx, slot, kind, owner=None, theta=None):
         self._ctx = ctx
@@ -43,6 +45,7 @@ class DeviceCache(object):
         self.kind = kind
         self._owner = owner  # the estimator (its kernel_func / X) for the K_chol refactor
         self._theta = None if theta is None else np.array(theta, dtype=np.float64)
+        self._kchol = None
 
     def __del__(self):
         try:
@@ -58,6 +61,8 @@ class DeviceCache(object):
         """chol(K(theta)) (n, n) lower, computed on the device (fp32-rounded read-back)."""
         if self.kind == _native.EST_PRIORMC:
             return self.read()[0]
+        if self._kchol is not None:
+            return self._kchol
         if self._owner is None or self._theta is None:
             raise ValueError('this cache does not record its theta')
         tmp = self._ctx.slots.acquire()
@@ -65,7 +70,8 @@ class DeviceCache(object):
             _, st, _ = self._owner._theta_call(_native.EST_PRIORMC, self._ctx, self._theta,
                                                _UBUF, tmp)
             _raise_for_status(int(st[0]), self._ctx)
-            return self._ctx.slot_read(tmp)[0]
+            self._kchol = self._ctx.slot_read(tmp)[0]
+            return self._kchol
         finally:
             self._ctx.slots.release(tmp)
 
@@ -76,7 +82,10 @@ class DeviceCache(object):
         return iter((self.k_chol(), L, f))
 
     def __array__(self, dtype=None, copy=None):
-        L = self.read()[0] if self.kind == _native.EST_PRIORMC else self.k_chol()
+        if self.kind != _native.EST_PRIORMC:
+            raise TypeError('an importance-sampling cache is the tuple (K_chol, C_chol, f_post), '
+                            'not an array: unpack it')
+        L = self.read()[0]
         return L if dtype is None else L.astype(dtype)
 
 

@@ -51,6 +51,14 @@ def parse():
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=30.0,
                     help='approximate seconds of CPU work for the baseline sample')
+    ap.add_argument('--parity', type=int, default=1,
+                    help='after the timed region: GPU theta-/u-calls vs the oracle (and the '
+                         "reference's own full-size fixture); exit 3 on a failure")
+    ap.add_argument('--ess-min', type=int, default=100,
+                    help='post-burn-in transitions per chain for the ESS (untimed extension)')
+    ap.add_argument('--ess-burn', type=int, default=50,
+                    help='transitions discarded from the start of each chain for the ESS '
+                         '(at least --warmup)')
     return ap.parse_args()
 
 
@@ -92,6 +100,27 @@ class Dist(object):
         t = self._t(x)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+    def all_gather(self, x):
+        """(world, *x.shape) float64 array of every rank's x (same shape on every rank)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if self.dist is None:
+            return x[None].copy()
+        import torch
+        t = torch.from_numpy(x.copy())
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.stack([o.numpy() for o in out])
+
+    def broadcast(self, x, src=0):
+        """rank src's float64 array x (shape known on every rank) on every rank."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.from_numpy(x.copy())
+        self.dist.broadcast(t, src)
+        return t.numpy()
 
     def close(self):
         if self.dist is not None:
@@ -203,32 +232,35 @@ def _blas_threads():
         return None
 
 
-def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, min_theta_calls=3):
+def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, U1, U2, min_theta_calls=3):
     """Time the CPU restatement (oracle/: C Gram + scipy LAPACK, the reference's op order) on a
-    bounded sample: >= 3 theta-calls and cached u-calls at the benchmark size, composed into
-    transitions/s of ONE chain with the per-transition call counts measured on the GPU run; plus
-    configs[0] (PM-MH, iso kernel, N=768 D=8, N_imp=1: one theta-call per MH iteration), the
-    reference's own CPU configuration. The port/reference calibration ratio measured in the
-    build container (tools/cpu_calibration.py -> profiles/r*_cpu_calibration.json) is attached."""
+    bounded sample: >= 3 theta-calls (draws U1) and cached u-calls (draws U2) at the benchmark
+    size, composed into transitions/s of ONE chain with the per-transition call counts measured
+    on the GPU run; plus configs[0] (PM-MH, iso kernel, N=768 D=8, N_imp=1: one theta-call per
+    MH iteration), the reference's own CPU configuration. The port/reference calibration ratio
+    measured in the build container (tools/cpu_calibration.py -> profiles/r*_cpu_calibration.json)
+    is attached. Also returns the first call pair's values: the oracle side of the parity check
+    at theta (the timing does not depend on which values are kept)."""
     import glob
-    sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import apm_oracle as orc
     from gpdemo.utils import synthetic_gp_data
     blas_threads = _blas_threads()
     est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
-    rng = np.random.RandomState(0)
-    ns = rng.normal(size=(X.shape[0], n_imp))
     t_theta, t_u = [], []
+    first = None
     t_start = time.perf_counter()
     while len(t_theta) < min_theta_calls or (time.perf_counter() - t_start < budget
                                              and len(t_theta) < 8):
+        ops0 = est.n_cubic_ops
         t0 = time.perf_counter()
-        _, cache = est(ns, theta)
+        v1, cache = est(U1, theta)
         t1 = time.perf_counter()
-        est(ns, None, cache)
+        v2, _ = est(U2, None, cache)
         t2 = time.perf_counter()
         t_theta.append(t1 - t0)
         t_u.append(t2 - t1)
+        if first is None:
+            first = (v1, v2, est.n_cubic_ops - ops0, np.array(cache[2]))
     tt, tu = float(np.median(t_theta)), float(np.median(t_u))
     per_transition = calls_theta * tt + calls_u * tu
     # configs[0]: PM-MH iso N=768 D=8 N_imp=1 (Pseudo-Marginal MH.ipynb protocol)
@@ -259,7 +291,7 @@ def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, min_theta_cal
                'reference_u_call_s': c2['reference']['u_call_s'],
                'configs0_ratio': c['configs0']['ratio_port_over_reference'],
                'configs0_reference_iters_per_s': c['configs0']['reference']['iters_per_s']}
-    return {
+    out = {
         'value': 1.0 / per_transition, 'unit': 'transitions/s (1 chain)',
         'cores': blas_threads if blas_threads else cores_visible, 'kind': 'port',
         'cores_note': ('BLAS threads = the CPU share this process is given (OMP_NUM_THREADS={0}); '
@@ -280,6 +312,175 @@ def cpu_baseline(X, y, n_imp, theta, calls_theta, calls_u, budget, min_theta_cal
                           'theta_call_s_median': float(np.median(t_c1))},
         'calibration': cal,
     }
+    return out, first
+
+
+# ------------------------------------------------------------------------------------ parity
+# After the timed region every rank evaluates, on its own GPU, one batched theta-call and one
+# cached u-call at two thetas (the bench theta*, and a long length-scale) on fixed draws, and
+# rank 0 compares them with the oracle (oracle/apm_oracle.py, estimators.py:152-241 in the
+# reference's op order) on the same inputs - and with the reference's own outputs at this size
+# (tests/golden/config2_ref.npz, made by tests/golden/make_golden_fullsize.py) when its data are
+# the bench's. A failed check makes bench.py exit 3 after printing its line.
+PARITY_TOL_NATS = 5e-4    # |d log f| of a theta-call / cached u-call
+PARITY_FPOST_REL = 1e-8   # max |d f_post| / max |f_post| (fp64-refined Newton modes)
+PARITY_U_SEED = 5         # U1, U2: the first two (N, S) normal draws of RandomState(5)
+REF_FIXTURE = os.path.join(REPO, 'tests', 'golden', 'config2_ref.npz')
+
+
+def parity_inputs(n, d, s):
+    base = np.log(np.sqrt(d))
+    thetas = np.stack([np.r_[0.0, np.full(d, base)],          # theta* (cpu_baseline's theta)
+                       np.r_[1.0, np.full(d, base + 2.0)]])   # long length-scale
+    rng = np.random.RandomState(PARITY_U_SEED)
+    return thetas, rng.normal(size=(n, s)), rng.normal(size=(n, s))
+
+
+def gpu_parity(X, y, n_imp, thetas, U1, U2, device):
+    """This rank's GPU values: batched theta-call (U1) + cached u-call (U2) at every theta."""
+    from gpdemo import _native
+    B = thetas.shape[0]
+    ctx = _native.Context(X, y, _native.KERNEL_ARD, 1e-8, n_imp, max_batch=B, n_slots=B,
+                          n_ubufs=2, device=device)
+    try:
+        ctx.u_upload(0, U1)
+        ctx.u_upload(1, U2)
+        v1, st1, nops = ctx.theta_eval(_native.EST_IS, thetas, [0] * B, list(range(B)))
+        v2, st2 = ctx.u_eval(list(range(B)), [1] * B)
+        fpost = np.stack([ctx.slot_read(b)[1] for b in range(B)])
+    finally:
+        ctx.close()
+    return v1, v2, nops.astype(np.float64), np.maximum(st1, st2).astype(np.float64), fpost
+
+
+def reference_fixture(X, y, n, d, s, seed):
+    """The reference's outputs at this workload (None when absent or another workload); the
+    bench's X must hash to the fixture's digest and its y equal the stored y."""
+    import hashlib
+    if not os.path.exists(REF_FIXTURE):
+        return None, 'absent'
+    z = np.load(REF_FIXTURE, allow_pickle=False)
+    if (int(z['n']), int(z['d']), int(z['s']), int(z['data_seed']), int(z['u_seed'])) != \
+            (n, d, s, seed, PARITY_U_SEED):
+        return None, 'another workload'
+    dig = hashlib.sha256(np.ascontiguousarray(X, dtype=np.float64).tobytes()).hexdigest()
+    if dig != str(z['x_sha256']) or not np.array_equal(z['y'].astype(np.float64), y):
+        return None, 'data differ on this host (X digest or y)'
+    return z, 'ok'
+
+
+def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
+    """GPU (every rank) vs oracle (rank 0, broadcast) and vs the reference fixture."""
+    import apm_oracle as orc
+    B, n = thetas.shape[0], X.shape[0]
+    g1, g2, gops, gst, gf = gpu_parity(X, y, a.n_imp, thetas, U1, U2, rank_device(dist))
+    orc_vals = np.zeros((B, 3))
+    orc_f = np.zeros((B, n))
+    t_orc = 0.
+    if dist.rank == 0:
+        t0 = time.perf_counter()
+        est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
+        for b in range(B):
+            if b == 0 and oracle_first is not None:  # cpu_baseline's first call pair
+                v1, v2, ops, f = oracle_first
+            else:
+                ops0 = est.n_cubic_ops
+                v1, cache = est(U1, thetas[b])
+                v2, _ = est(U2, None, cache)
+                ops, f = est.n_cubic_ops - ops0, cache[2]
+            orc_vals[b] = (v1, v2, ops)
+            orc_f[b] = f
+        t_orc = time.perf_counter() - t0
+    orc_vals = dist.broadcast(orc_vals)
+    orc_f = dist.broadcast(orc_f)
+    fscale = np.abs(orc_f).max(1)
+    mine = np.concatenate([g1 - orc_vals[:, 0], g2 - orc_vals[:, 1], gops - orc_vals[:, 2], gst,
+                           np.abs(gf - orc_f).max(1) / fscale, g1, g2])
+    allr = dist.all_gather(mine)  # (world, 7B)
+    d1, d2, dops, st, frel = (allr[:, k * B:(k + 1) * B] for k in range(5))
+    out = {'thetas': ['theta* (log sigma 0, log tau_k log sqrt(D))',
+                      'long length-scale (log sigma 1, log tau_k log sqrt(D) + 2)'],
+           'draws': 'U1, U2 = first two (N, N_imp) normal draws of RandomState({0}); theta-call '
+                    'on U1, cached u-call on U2'.format(PARITY_U_SEED),
+           'checked_ranks': int(dist.world),
+           'd_theta_call': float(np.abs(d1).max()), 'd_u_call': float(np.abs(d2).max()),
+           'd_theta_call_per_theta': np.abs(d1).max(0).tolist(),
+           'd_u_call_per_theta': np.abs(d2).max(0).tolist(),
+           'n_cubic_ops_equal': bool((dops == 0).all()),
+           'status_ok': bool((st == 0).all()),
+           'f_post_max_rel': float(frel.max()),
+           'tol': {'abs_nats': PARITY_TOL_NATS, 'f_post_rel': PARITY_FPOST_REL},
+           'oracle': {'theta_call': orc_vals[:, 0].tolist(), 'u_call': orc_vals[:, 1].tolist(),
+                      'n_cubic_ops': orc_vals[:, 2].astype(int).tolist(),
+                      'seconds': t_orc if dist.rank == 0 else None}}
+    ok = (out['d_theta_call'] <= PARITY_TOL_NATS and out['d_u_call'] <= PARITY_TOL_NATS and
+          out['n_cubic_ops_equal'] and out['status_ok'] and out['f_post_max_rel'] <= PARITY_FPOST_REL)
+    z, why = reference_fixture(X, y, a.n, a.d, a.n_imp, a.seed)
+    ref = {'fixture': os.path.relpath(REF_FIXTURE, REPO), 'used': z is not None, 'why': why}
+    if z is not None:
+        gv1 = allr[:, 5 * B:6 * B]
+        gv2 = allr[:, 6 * B:7 * B]
+        r1, r2 = z['logf1'][:B], z['logf2'][:B]
+        rf = z['f_post'][:B]
+        ref.update({
+            'reference_theta_call': r1.tolist(), 'reference_u_call': r2.tolist(),
+            'd_theta_call': float(np.abs(gv1 - r1).max()),
+            'd_u_call': float(np.abs(gv2 - r2).max()),
+            'n_cubic_ops_equal': bool((orc_vals[:, 2] == z['n_cubic_ops'][:B]).all() and
+                                      (dops == 0).all()),
+            'oracle_minus_reference': {
+                'theta_call': float(np.abs(orc_vals[:, 0] - r1).max()),
+                'u_call': float(np.abs(orc_vals[:, 1] - r2).max()),
+                'f_post_max_rel': float((np.abs(orc_f - rf).max(1) /
+                                         np.abs(rf).max(1)).max())}})
+        # the GPU's f_post vs the reference's: oracle's (checked above) within its own pin
+        ok = ok and ref['d_theta_call'] <= PARITY_TOL_NATS and \
+            ref['d_u_call'] <= PARITY_TOL_NATS and ref['n_cubic_ops_equal']
+    out['vs_reference'] = ref
+    out['pass'] = bool(ok)
+    return out
+
+
+def ess_block(dist, smp, series, done, burn, elapsed, P):
+    """ESS on theta per the reference's analysis protocol (Analyse
+    results.ipynb:138-141, coda effectiveSize / gelman.diag restated in auxpm/diagnostics.py):
+    each live chain's series after `burn` discarded transitions (>= ess-min of them, the chain
+    extended untimed past the timed region where needed); ESS per transition = min over the
+    theta components of ESS / length; ess_per_sec = sum over chains of that x the chain's timed
+    transitions / the timed wall time (= ESS per transition x transitions/s). R-hat over this
+    rank's chains on their common length."""
+    from auxpm.diagnostics import effective_size, gelman_rubin
+    live = [c for c in range(smp.n_chains) if not smp.failed[c] and len(series[c]) > burn + 3]
+    e_min, e_mean, lens = [], [], []
+    for c in live:
+        x = np.array(series[c][burn:])
+        e = effective_size(x)
+        e_min.append(e.min() / len(x))
+        e_mean.append(e.mean() / len(x))
+        lens.append(len(x))
+    w = np.array([done[c] for c in live], dtype=np.float64)
+    ess_ps = dist.sum(float(np.dot(e_min, w))) / elapsed
+    ess_mean_ps = dist.sum(float(np.dot(e_mean, w))) / elapsed
+    n_chains = dist.sum(len(live))
+    rhat = None
+    if len(live) >= 2:
+        L = min(lens)
+        r = gelman_rubin(np.stack([np.array(series[c][burn:burn + L]) for c in live]))
+        rhat = {'max': dist.max(float(r.max())), 'median_rank0': float(np.median(r)),
+                'length': int(L), 'chains_per_rank': len(live)}
+    return {'ess_per_sec': ess_ps, 'ess_mean_per_sec': ess_mean_ps, 'rhat': rhat,
+            'sample': {
+                'chains': int(n_chains),
+                'burn_in_discarded': int(burn),
+                'post_burn_transitions_per_chain_min': int(-dist.max(-min(lens or [0]))),
+                'post_burn_transitions_per_chain_max': int(dist.max(max(lens or [0]))),
+                'ess_per_transition_mean': dist.sum(float(np.sum(e_min))) / max(1., n_chains),
+                'method': 'coda effectiveSize restatement (auxpm/diagnostics.py) per chain on '
+                          'its series after the burn-in (warm-up + timed + untimed extension '
+                          'transitions of the same chain), min over the {0} theta components, '
+                          'divided by the series length; x the chain\'s timed transitions, '
+                          'summed over chains and ranks, / timed wall time. R-hat: coda '
+                          'gelman.diag restatement, max over components (and ranks)'.format(P)}}
 
 
 def main():
@@ -290,24 +491,30 @@ def main():
                          'torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr '
                          '127.0.0.1 --master-port P bench.py --gpus N`'.format(a.gpus, dist.world))
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
-    from auxpm.diagnostics import effective_size
     from gpdemo import _native
     from gpdemo.utils import synthetic_gp_data
 
-    _SYNC_DEVICE[0] = rank_device(dist)
+    dev = rank_device(dist)
+    _SYNC_DEVICE[0] = dev
     X, y = synthetic_gp_data(a.n, a.d, a.seed)
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
-        seed=chain_seed(a.seed, dist.rank), device=rank_device(dist))
+        seed=chain_seed(a.seed, dist.rank), device=dev)
     P = smp.P
     smp.initialise()
+    series = [[] for _ in range(a.chains)]  # every transition of each chain (ESS)
     if a.schedule == 'async':
         if a.warmup:
-            smp.run_async(a.warmup)  # every chain W transitions, ending on a transition boundary
+            # every chain W transitions, ending on a transition boundary
+            wtr, _ = smp.run_async(a.warmup)
+            for c in range(a.chains):
+                series[c].extend(wtr[c])
     else:
         for _ in range(a.warmup):
-            smp.step()
+            th = smp.step()
+            for c in range(a.chains):
+                series[c].append(th[c].copy())
     ctx = smp.ctx
     for k in range(_native.PROF_NKINDS):
         ctx.prof_read(k, reset=True)
@@ -331,24 +538,27 @@ def main():
             res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
         elapsed = timed_region(dist, body, 1, mark)
         done = res['done']
-        # every completed timed transition of each live chain (>= K per chain)
-        tr_list = [np.array(res['traces'][c]) for c in range(a.chains)
-                   if not smp.failed[c] and done[c] >= a.steps]
+        for c in range(a.chains):
+            series[c].extend(res['traces'][c])
     else:
-        thetas = []
-
         def one_step():
-            thetas.append(smp.step())
+            th = smp.step()
+            for c in range(a.chains):
+                series[c].append(th[c].copy())
         elapsed = timed_region(dist, one_step, a.steps, mark)
         done = np.where(smp.failed, 0, a.steps)
-        tr_list = [np.stack(thetas, 1)[c] for c in range(a.chains) if not smp.failed[c]]
     ctx.prof_marker(2)
     ctx.prof_enable(False)
-    local_tr = int(done[~smp.failed].sum())
+    done = np.where(smp.failed, 0, done)
+    local_tr = int(done.sum())
+    local_elapsed = elapsed
     transitions = dist.sum(local_tr)
     value = transitions / elapsed
     n_th = (smp.n_theta_calls - th0) / max(1, local_tr)
     n_u = (smp.n_u_calls - u0) / max(1, local_tr)
+    call_ops = list(smp.call_ops)
+    wall = dict(smp.wall)
+    batch_hist = {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()}
 
     prof = {}
     for k, name in ((_native.PROF_GRAM, 'gram'), (_native.PROF_CHOL_UPDATE_OUTER, 'chol_update'),
@@ -357,6 +567,7 @@ def main():
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
     _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
+    _, n_df_timeouts, _ = ctx.prof_read(_native.PROF_DF_TIMEOUTS, reset=True)
 
     def mfma_roofline(name, kernel, peak, shorts, kind):
         ms, cnt, flops = prof[name]
@@ -415,39 +626,56 @@ def main():
         mf = pmc_mfma('f32', 'k_ugemm')
         if mf:
             extra['roofline_lu']['mfma_busy'] = mf
-    # ESS/s on theta (Analyse results.ipynb:138-139 uses coda's effectiveSize):
-    # sum over chains of min over theta components of the chain's ESS over ALL its completed
-    # timed transitions, / the timed wall time. Defined for any K (the driver runs K=20); with few
-    # transitions per chain after a short warm-up the AR(p) fit is noisy, so the sample is stated.
-    ess_c = [effective_size(t) for t in tr_list if len(t) >= 4]
-    n_per_chain = [len(t) for t in tr_list]
-    n_ess = dist.sum(len(ess_c))  # collectives on every rank, whatever its local sample
-    ess_min_sum = dist.sum(sum(e.min() for e in ess_c))
-    ess_mean_sum = dist.sum(sum(e.mean() for e in ess_c))
-    ess_per_sec = ess_min_sum / elapsed if n_ess else None
-    ess_mean_per_sec = ess_mean_sum / elapsed if n_ess else None
-    ess_first_k = None
-    if a.steps >= 100:  # the round-1 definition: each chain's first K timed transitions only
-        ess_first_k = dist.sum(sum(effective_size(t[:a.steps]).min() for t in tr_list)) / elapsed
-    ess_sample = {'chains': int(n_ess),
-                  'transitions_per_chain_min': int(-dist.max(-min(n_per_chain or [0]))),
-                  'transitions_per_chain_max': int(dist.max(max(n_per_chain or [0]))),
-                  'transitions_per_chain_mean': dist.sum(sum(n_per_chain)) /
-                  max(1., dist.sum(len(n_per_chain))),
-                  'warmup_transitions_discarded': a.warmup,
-                  'estimator': 'coda effectiveSize restatement (auxpm/diagnostics.py), per chain '
-                               'min over the {0} theta components, summed over chains'.format(P)}
 
-    cpu = None
+    # ESS: extend the same chains (untimed) until each has >= ess-min transitions after the
+    # burn-in, then ESS per transition x the timed transitions/s (ess_block)
+    burn = max(a.ess_burn, a.warmup)
+    need = np.array([0 if smp.failed[c] else max(0, burn + a.ess_min - len(series[c]))
+                     for c in range(a.chains)], dtype=np.int64)
+    t_ext = time.perf_counter()
+    if need.max() > 0 and a.schedule == 'async':
+        etr, _ = smp.run_async(need)
+        for c in range(a.chains):
+            series[c].extend(etr[c])
+    elif need.max() > 0:
+        for _ in range(int(need.max())):
+            th = smp.step()
+            for c in range(a.chains):
+                series[c].append(th[c].copy())
+    t_ext = time.perf_counter() - t_ext
+    ess = ess_block(dist, smp, series, done, burn, elapsed, P)
+    ess['sample']['untimed_extension_s_rank0'] = t_ext
+    ess["sample"]["timed_transitions_per_chain_min"] = int(-dist.max(
+        -(done[~smp.failed].min() if (~smp.failed).any() else 0)))
+    ess['sample']['timed_transitions_per_chain_max'] = int(dist.max(done.max()))
+    failed = int(dist.sum(int(smp.failed.sum())))
+    ctx.close()  # frees the chains' workspaces before the parity context
+
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    cpu, first = None, None
+    thetas_par, U1, U2 = parity_inputs(a.n, a.d, a.n_imp)
     if a.cpu_baseline and dist.rank == 0:
-        theta_ref = np.r_[0.0, np.full(a.d, np.log(np.sqrt(a.d)))]
-        cpu = cpu_baseline(X, y, a.n_imp, theta_ref, n_th, n_u, a.cpu_budget)
+        cpu, first = cpu_baseline(X, y, a.n_imp, thetas_par[0], n_th, n_u, a.cpu_budget, U1, U2)
         cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
+    parity = parity_check(dist, X, y, a, thetas_par, U1, U2, first) if a.parity else None
+
+    # per-rank record: device, chains, transitions, elapsed (8 distinct devices, even load)
+    mine = np.array([float(dist.rank), float(dev), float(a.chains), float(local_tr),
+                     float(local_elapsed), float(int(smp.failed.sum()))])
+    ranks = [{'rank': int(r[0]), 'device': int(r[1]), 'chains': int(r[2]),
+              'transitions': int(r[3]), 'elapsed_s': r[4], 'failed_chains': int(r[5]),
+              'transitions_per_s': r[3] / r[4]} for r in dist.all_gather(mine)]
 
     line = {
         'metric': METRIC, 'value': value, 'unit': 'transitions/s (all chains, all GPUs)',
         'n_gpus': dist.world, 'steps': a.steps, 'warmup': a.warmup,
-        'ms_per_step': 1e3 * elapsed / a.steps, 'higher_is_better': True, 'scaling': 'weak',
+        'ms_per_step': 1e3 * elapsed / a.steps,
+        'ms_per_step_note': 'timed wall time / --steps; under the asynchronous schedule every '
+                            'chain completes >= --steps transitions (chains ahead keep working), '
+                            'so this is neither a lockstep step time nor a per-transition time: '
+                            'see ms_per_transition_per_chain',
+        'ms_per_transition_per_chain': 1e3 * elapsed * a.chains * dist.world / max(1, transitions),
+        'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None, 'dtype': 'mixed f64/f32',
         'dtype_detail': 'theta-path Gram, chol(K) and the posterior-covariance factor fp64 on f64 '
                         'MFMA; Newton matrix B factored in fp32 (trailing updates fp16x3: fp16 '
@@ -462,29 +690,35 @@ def main():
                    'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
                    .format(dist.world)},
-        'ess_per_sec': ess_per_sec, 'ess_mean_per_sec': ess_mean_per_sec,
-        'ess_per_sec_first_k': ess_first_k, 'ess_sample': ess_sample,
+        'ess_per_sec': ess['ess_per_sec'], 'ess_mean_per_sec': ess['ess_mean_per_sec'],
+        'rhat': ess['rhat'], 'ess_sample': ess['sample'],
+        'parity': parity,
         'schedule': a.schedule, 'transitions_timed': int(transitions),
         'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
-        'failed_chains': int(dist.sum(int(smp.failed.sum()))),
+        'failed_chains': failed,
         'newton_refinement_steps': int(dist.sum(n_refine)),
         'newton_fp64_reruns': int(dist.sum(n_rerun)),
+        'newton_dataflow_spin_timeouts': int(dist.sum(n_df_timeouts)),
         'cubic_ops_per_theta_call': {
-            'mean_of_batch_max': float(np.mean([m for m, _ in smp.call_ops])) if smp.call_ops
-            else None,
-            'mean_of_batch_mean': float(np.mean([a for _, a in smp.call_ops])) if smp.call_ops
-            else None,
+            'mean_of_batch_max': float(np.mean([m for m, _ in call_ops])) if call_ops else None,
+            'mean_of_batch_mean': float(np.mean([v for _, v in call_ops])) if call_ops else None,
             'note': 'IS: Newton iterations + 3 (estimators.py:217); a batched call lasts as long '
                     'as its slowest chain'},
-        'wall_split_s': dict(smp.wall, host_sampler=elapsed - sum(smp.wall.values())),
-        'calls_by_batch_size': {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()},
+        'wall_split_s': dict(wall, host_sampler=elapsed - sum(wall.values())),
+        'calls_by_batch_size': batch_hist,
+        'ranks': ranks,
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
+    ok = parity is None or parity['pass']
     dist.close()
     del _native
+    if not ok:
+        if dist.rank == 0:
+            print('bench.py: PARITY FAILED (see the "parity" block)', file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == '__main__':

@@ -98,6 +98,16 @@ int apm_theta_eval_K(apm_ctx *ctx, int estimator, const double *K, int64_t ldk, 
 /* cached u-call: reuse slots[i]'s per-theta state with draws ubufs[i] */
 int apm_u_eval(apm_ctx *ctx, int64_t count, const int64_t *slots, const int64_t *ubufs,
                double *out_logf, int *status);
+/* cache-slot lifetimes (samplers.py:563-584: an MH sampler keeps the current state's cache and the
+ * proposal's alive at once). acquire: a free slot, one owner (APM_E_NOMEM when all are owned);
+ * copy: one more owner of the same (immutable) state - the handle copy of the reference's tuple;
+ * release: one owner fewer, the slot is free again at zero (APM_E_INVALID if not acquired);
+ * refcount: owners of a slot (negative on a bad argument). Host bookkeeping, no device work.
+ * apm_theta_eval / apm_u_eval take any slot index; the Python layer allocates through these. */
+int apm_cache_acquire(apm_ctx *ctx, int64_t *slot);
+int apm_cache_copy(apm_ctx *ctx, int64_t slot);
+int apm_cache_release(apm_ctx *ctx, int64_t slot);
+int64_t apm_cache_refcount(const apm_ctx *ctx, int64_t slot);
 /* read a slot back (any pointer may be NULL): factor (n x n lower, fp32 rounded), f_post, g, cst */
 int apm_slot_read(apm_ctx *ctx, int64_t slot, double *L, int64_t ldl, double *f_post, double *g,
                   double *cst);
@@ -120,7 +130,11 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
                             rerun in fp64, work = refinement steps launched, total_ms = 0 */
 #define APM_PROF_CHOL_UPDATE32_OUTER 5 /* the rank-64*OUTER launches among CHOL_UPDATE32 */
 #define APM_PROF_CHOL_UPDATE_OUTER 6   /* the rank-64*OUTER launches among CHOL_UPDATE */
-#define APM_PROF_NKINDS 7
+#define APM_PROF_DF_TIMEOUTS 7 /* not a kernel: launches = bounded-spin timeouts of the Newton
+                                 factorisation's dataflow panel launches (each fails its chain,
+                                 which the Newton loop reruns in fp64; apart from breakdowns of
+                                 the fp32 factor, which are not counted here) */
+#define APM_PROF_NKINDS 8
 /* on = 0 off; 1 the roofline kinds (GRAM, UGEMM and the two *_OUTER kinds: one event pair per
  * launch of those kernels only, so that the timing adds little to a timed region); 2 every kind
  * (CHOL_UPDATE / CHOL_UPDATE32 add an event pair around every in-panel update launch) */

@@ -2,20 +2,20 @@
 
 * configs[2] — N=4096 D=32 ARD-SE, N_imp=256: one batched theta-call of 4 chains (the bench's
   theta*, a long length-scale, sigma = e^18.5 next to the fp16x3 guard, a prior-like draw) and a
-  cached u-call, against the oracle's CPU restatement of estimators.py:152-241 on the same
-  (theta, u). This is the size the bench runs, with its multi-panel fp16x3 Newton updates, the
+  cached u-call, against the REFERENCE's own outputs on the same (theta, u)
+  (tests/golden/config2_ref.npz, made by tests/golden/make_golden_fullsize.py). This is the size the bench runs, with its multi-panel fp16x3 Newton updates, the
   4-workgroup TRSV, the concurrent chol(K) and the single-launch SYRK.
-* configs[4] — N=16384 D=64 N_imp=1024: the default path against the all-fp32-operand
-  (APM_H3=0) and all-fp64 Newton (APM_MIXED=0) paths on the same inputs (the oracle would take
-  ~10 CPU-minutes here), plus the oracle itself at N=8192 (tools/stress.py's check, as a test).
+* configs[4] — N=16384 D=64 N_imp=1024: against the REFERENCE's own outputs at full size
+  (tests/golden/config4_ref.npz), and the default path against the all-fp32-operand (APM_H3=0)
+  and all-fp64 Newton (APM_MIXED=0) paths on the same inputs.
 * configs[0] — PM-MH, iso kernel, N=768 D=8, N_imp=1, Laplace-estimator adaptive phase then the
   IS main phase (Pseudo-Marginal MH.ipynb cells 12-14): the reference's own chain
   (tests/golden/pmmh_chain.npz) replayed with the GPU estimators and the API-compatible
   PMMHSampler, call by call.
 
-Tolerance for estimator values: |d log f| <= 1e-3 + 2e-7 |log f| (the fp32 L.U
-and epilogue; measured 1e-4 .. 2e-4 at N=4096..8192). n_cubic_ops must be equal and f_post
-within 1e-9 relative (fp64 Newton modes).
+Tolerance for estimator values: |d log f| <= 5e-4 nats absolute, for every
+theta including sigma = e^18.5 where |log f| = 2e10 (the fp32 L.U and epilogue). n_cubic_ops must
+be equal and f_post within 1e-8 of its maximum (fp64-refined Newton modes).
 """
 import os
 import sys
@@ -30,11 +30,12 @@ from conftest import golden
 
 pytestmark = pytest.mark.gpu
 
-TOL_ABS, TOL_REL = 1e-3, 2e-7
+TOL_NATS = 5e-4   # |d log f| of every theta-call / u-call, no relative term
+FPOST_REL = 1e-8  # max |d f_post| / max |f_post|
 
 
 def _tol(r):
-    return TOL_ABS + TOL_REL * abs(r)
+    return TOL_NATS
 
 
 @pytest.fixture(scope='module')
@@ -65,45 +66,68 @@ class _Heartbeat(object):
         self.done.set()
 
 
-def config2_thetas(d):
-    base = np.log(np.sqrt(d))
-    rng = np.random.RandomState(2024)
-    return np.stack([np.r_[0.0, np.full(d, base)],                        # bench theta*
-                     np.r_[1.0, np.full(d, base + 2.0)],                  # long length-scale
-                     np.r_[18.5, rng.normal(scale=0.2, size=d) + base - 0.5],  # fp16x3 guard edge
-                     np.r_[0.7, rng.normal(scale=0.5, size=d) + base]])   # prior-like
+def _fixture(name, X, y):
+    """The reference's own outputs at a BASELINE configuration (tests/golden/
+    make_golden_fullsize.py); refuses when this host's data differ from the fixture's."""
+    import hashlib
+    z = golden(name)
+    assert hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest() == str(z['x_sha256']), \
+        'X differs from the fixture data (numpy RandomState / normalise_inputs changed?)'
+    np.testing.assert_array_equal(z['y'].astype(np.float64), y)
+    return z
 
 
-def test_config2_full_size_vs_oracle(nat):
-    from gpdemo.utils import synthetic_gp_data
-    n, d, s = 4096, 32, 256
-    X, y = synthetic_gp_data(n, d, 20151009)
-    th = config2_thetas(d)
+def _vs_reference(nat, X, y, z, s, u_seed, max_batch):
+    n = X.shape[0]
+    th = z['thetas']
     B = th.shape[0]
-    rng = np.random.RandomState(5)
+    rng = np.random.RandomState(u_seed)
     U1, U2 = rng.normal(size=(n, s)), rng.normal(size=(n, s))
-    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=B, n_slots=B, n_ubufs=2)
-    ctx.u_upload(0, U1)
-    ctx.u_upload(1, U2)
-    out, st, nops = ctx.theta_eval(nat.EST_IS, th, [0] * B, list(range(B)))
-    out2, st2 = ctx.u_eval(list(range(B)), [1] * B)
-    fpost = [ctx.slot_read(b)[1] for b in range(B)]
-    ctx.close()
-    assert (st == 0).all() and (st2 == 0).all(), (st, st2)
-    kf = orc.make_kernel_func('ard', 1e-8)
-    K = np.empty((n, n))
+    out, out2, nops, fpost, cld = [], [], [], [], []
+    for b0 in range(0, B, max_batch):
+        bb = list(range(b0, min(B, b0 + max_batch)))
+        ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=len(bb), n_slots=len(bb),
+                          n_ubufs=2)
+        ctx.u_upload(0, U1)
+        ctx.u_upload(1, U2)
+        o, st, nop = ctx.theta_eval(nat.EST_IS, th[bb], [0] * len(bb), list(range(len(bb))))
+        o2, st2 = ctx.u_eval(list(range(len(bb))), [1] * len(bb))
+        assert (st == 0).all() and (st2 == 0).all(), (st, st2)
+        for q in range(len(bb)):
+            L, f, _, _ = ctx.slot_read(q)
+            fpost.append(f)
+            cld.append(np.log(np.diagonal(L)))
+        ctx.close()
+        out += list(o)
+        out2 += list(o2)
+        nops += list(nop)
     report = []
-    with _Heartbeat('configs[2] oracle'):
-        for b in range(B):
-            r1, rc, cubic = orc.is_estimate(X, y, kf, U1, th[b], K_work=K)
-            r2, _, _ = orc.is_estimate(X, y, kf, U2, None, rc)
-            report.append((b, out[b] - r1, out2[b] - r2))
-            assert nops[b] == cubic, (b, nops[b], cubic)
-            assert abs(out[b] - r1) <= _tol(r1), (b, out[b], r1)
-            assert abs(out2[b] - r2) <= _tol(r2), (b, out2[b], r2)
-            np.testing.assert_allclose(fpost[b], rc[2], rtol=1e-9,
-                                       atol=1e-9 * np.abs(rc[2]).max())
-    print('configs[2] d(theta-call), d(u-call):', report)
+    for b in range(B):
+        assert int(z['status'][b]) == 0, 'the reference failed at this theta'
+        d1, d2 = out[b] - z['logf1'][b], out2[b] - z['logf2'][b]
+        report.append((b, d1, d2))
+        tol = TOL_NATS
+        assert nops[b] == int(z['n_cubic_ops'][b]), (b, nops[b], z['n_cubic_ops'][b])
+        assert abs(d1) <= tol, (b, out[b], z['logf1'][b])
+        assert abs(d2) <= tol, (b, out2[b], z['logf2'][b])
+        fr = z['f_post'][b]
+        np.testing.assert_allclose(fpost[b], fr, rtol=0, atol=FPOST_REL * np.abs(fr).max())
+        # C_chol's diagonal (fp32 in the slot): log-diagonal to fp32 resolution
+        np.testing.assert_allclose(cld[b], z['c_logdiag'][b], rtol=0, atol=2e-6)
+    return report
+
+
+def test_config2_full_size_vs_reference(nat):
+    """configs[2] at full size against the REFERENCE's own outputs (tests/golden/config2_ref.npz:
+    the reference estimator run on these inputs in the build container; the oracle equals it
+    bit for bit there): 4 thetas in one batched call — the bench's theta*, a long length-scale,
+    sigma = e^18.5 next to the fp16x3 guard (|log f| = 2e10), a prior-like draw."""
+    from gpdemo.utils import synthetic_gp_data
+    z = golden('config2_ref')
+    X, y = synthetic_gp_data(int(z['n']), int(z['d']), int(z['data_seed']))
+    z = _fixture('config2_ref', X, y)
+    rep = _vs_reference(nat, X, y, z, int(z['s']), int(z['u_seed']), 4)
+    print('configs[2] vs reference d(theta-call), d(u-call):', rep)
 
 
 def _stress_data(n, d, seed):
@@ -127,6 +151,18 @@ def _run(nat, X, y, th, s, U, monkeypatch, **env):
     f = [ctx.slot_read(b)[1] for b in range(B)]
     ctx.close()
     return out, st, nops, out2, f
+
+
+def test_config4_full_size_vs_reference(nat):
+    """configs[4] at full size, N=16384 D=64 N_imp=1024, against the REFERENCE's own outputs
+    (tests/golden/config4_ref.npz; the reference's theta-call takes ~15 CPU-minutes each here):
+    two thetas in one batched call, theta-call + cached u-call values, n_cubic_ops, f_post and
+    C_chol's diagonal."""
+    z = golden('config4_ref')
+    X, y = _stress_data(int(z['n']), int(z['d']), int(z['data_seed']))
+    z = _fixture('config4_ref', X, y)
+    rep = _vs_reference(nat, X, y, z, int(z['s']), int(z['u_seed']), 2)
+    print('configs[4] vs reference d(theta-call), d(u-call):', rep)
 
 
 def test_config4_full_size_paths_agree(nat, monkeypatch):
@@ -234,7 +270,7 @@ def test_config0_pmmh_chain_matches_reference(nat):
     imp.reset_cubic_op_count()
     thetas, n_reject = sampler.get_samples(ath[-1], g['thetas'].shape[0])
     dv = np.abs(np.array(calls[na:]) - g['calls'][na:])
-    assert (dv <= TOL_ABS + TOL_REL * np.abs(g['calls'][na:])).all(), dv.max()
+    assert (dv <= TOL_NATS).all(), dv.max()
     np.testing.assert_array_equal(thetas, g['thetas'])
     assert n_reject == int(g['n_reject'])
     assert imp.n_cubic_ops == int(g['n_cubic_ops'])
