@@ -40,6 +40,16 @@ __device__ __forceinline__ float log_ndtr_f(float z) {
     return log1pf(-0.5f * erfcf(z * rs2));
 }
 
+// log Phi(z) with the -z^2/2 of the negative branch in fp64 and the O(log|z|) remainder in fp32
+// (the u-path epilogue, ugemm.hip: the large terms of the per-sample sum cancel in fp64; the
+// fp32 part is bounded by ~1 + log|z| in magnitude, so its rounding stays below 1e-6 per entry)
+__device__ __forceinline__ double log_ndtr_mixed(double z) {
+    const float rs2 = 0.70710678118654752440f;
+    const float zf = (float)z;
+    if (z < 0.0) return (double)__logf(0.5f * erfcxf(-zf * rs2)) - 0.5 * z * z;
+    return (double)log1pf(-0.5f * erfcf(zf * rs2));
+}
+
 // wave64 reductions
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll

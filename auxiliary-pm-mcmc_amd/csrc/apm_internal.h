@@ -169,15 +169,28 @@ void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet
                         int64_t lstride, int nb, double* out, Live live, int nchains,
                         hipStream_t s);
 
-// cache slot: fp32 factor with an extra TB-row block (row np holds g^T), plus vectors
+// cache slot: fp32 factor with an extra TB-row block (row np holds g^T for apm_slot_read; the
+// estimate does not use it), plus fp64 vectors of the self-consistent epilogue (ugemm.hip)
 struct SlotSet {
     float* L;           // (np + TB) x np, ld = np
-    float* fpost;       // np
-    float* W;           // np
-    double* fpost64;    // np
-    double* cst;        // 1 per slot: -1/2|g|^2 - 1/2 log|B|  (0 for PriorMC)
+    double* fpost64;    // np: f_post
+    double* W64;        // np: W of the last Newton iteration (0 for PriorMC)
+    double* z64;        // np: z = C^-1 f_post = a + W f_post (0 for PriorMC)
+    double* cst;        // 1 per slot: 1/2 f_post^T z - 1/2 log|B|  (0 for PriorMC)
     int64_t lstride, vstride;
+    // wide slots (trace of the factor's Gram L L^T above APM_WIDE_Q, ugemm.hip): the factor is
+    // also kept in fp64 and their u-path runs on f64 MFMA
+    double* L64;        // np x np per wide slot, ld = np (stride l64stride)
+    double* rowq;       // np per slot: squared row norms of the factor (k_slot_write_L)
+    int* wide;          // 1 per slot
+    int* chain_wide;    // 1 per chain of the call (read back with the theta-call's results)
+    int64_t l64stride;
+    double wide_q;      // the threshold (APM_WIDE_Q, overridable by the environment variable)
 };
+// trace(L L^T) above which a slot's u-path runs in fp64: the fp32 L.U moves
+// log f by ~1e-10 x trace (11 nats at trace 1.15e11, sigma = e^18.5; < 1e-6 nats at the trace
+// ~1e3 of typical thetas), so this keeps the fp32 rounding of L and U below ~1e-4 nats
+#define APM_WIDE_Q 1.0e6
 // write slot slots[b] from the factored work matrix. mode 0 = IS via the augmented matrix (C_chol
 // at offset (np,np), g in row 2np), mode 1 = PriorMC (K_chol at (0,0), g = 0), mode 2 = IS via
 // chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb)
@@ -205,15 +218,16 @@ void launch_merge_status(int* status, const int* other, int code, int nchains, h
 // ---- newton.hip: read-back of up to three small device arrays (4-byte words) into mapped
 // pinned host memory, back to back at dst (device address of the host buffer)
 struct Export {
-    const unsigned* src[3];
-    int words[3];
+    const unsigned* src[4];
+    int words[4];
     unsigned* dst;
 };
 void launch_export(const Export& e, hipStream_t s);
 
 // ---- ugemm.hip ------------------------------------------------------------------------------
 struct UPool {
-    float* base;        // each buffer: np x sp fp32, ld = sp, zero padded
+    double* base;       // each buffer: np x sp fp64, ld = sp, zero padded (device normals are
+                        // fp32 values; host uploads keep their fp64 values for the wide path)
     int64_t stride;
     int sp;
 };
@@ -225,9 +239,10 @@ void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64
                       const double* ca, const double* cb, int n, int S, int nchains,
                       hipStream_t s);
 // partial[b][i][s] = sum over rows of row-block i of t(n,s) (i < nb), partial[b][nb][s] = g^T u_s
+// wide: also launch the f64 MFMA twin for the call's wide slots (k_ugemm64)
 void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
                   const double* y, int n, int np, double* partial, int64_t pstride,
-                  const int* status, int nchains, hipStream_t s);
+                  const int* status, int nchains, bool wide, hipStream_t s);
 void launch_lme(const double* partial, int64_t pstride, int nb, int S, int sp, SlotSet Sl,
                 const int64_t* slots, double* out, const int* status, int nchains,
                 hipStream_t s);

@@ -37,6 +37,7 @@ struct apm_ctx {
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
     std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
+    std::vector<int> slot_wide;  // host mirror of Sl.wide (read back with each theta-call)
     double eps = 1e-8, tol = 1e-4;
     int64_t max_iters = 1000;
     std::string err;
@@ -504,11 +505,13 @@ void upload_h3(apm_ctx* c, int count) {
     HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
 }
 
-void u_eval_device(apm_ctx* c, int count) {
+// wide: some slot of the call may be wide (theta-calls: unknown until the read-back; u-calls:
+// the host mirror) - the f64 MFMA twin is launched as well
+void u_eval_device(apm_ctx* c, int count, bool wide) {
     {
         ProfScope ps(c, APM_PROF_UGEMM, (double)c->n * (c->n + 1) * c->S * count);
         launch_ugemm(c->Sl, c->d_slots, c->Up, c->d_ubufs, c->y, c->n, c->np, c->partial,
-                     c->pstride, c->status, count, c->stream);
+                     c->pstride, c->status, count, wide, c->stream);
         check_launch();
     }
     launch_lme(c->partial, c->pstride, c->nb, c->S, c->sp, c->Sl, c->d_slots, c->out, c->status,
@@ -847,7 +850,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 1, c->n,
                           c->np, lv, count, c->stream);
         check_launch();
-        u_eval_device(c, count);
+        u_eval_device(c, count, true);
     } else {
         if (ov) {
             HIPC(hipEventRecord(c->ev_gram, c->stream));
@@ -883,12 +886,23 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, mode,
                               c->n, c->np, lv, count, c->stream);
             check_launch();
-            u_eval_device(c, count);
+            u_eval_device(c, count, true);
         }
     }
-    read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
-                  RB{c->status, (int)sizeof(int) * count, st_h.data()},
-                  RB{c->n_iter, (int)sizeof(int) * count, it_h.data()}});
+    std::vector<int> wide_h(count, 0);
+    if (est == APM_EST_LAPLACE) {
+        read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
+                      RB{c->status, (int)sizeof(int) * count, st_h.data()},
+                      RB{c->n_iter, (int)sizeof(int) * count, it_h.data()}});
+    } else {
+        read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
+                      RB{c->status, (int)sizeof(int) * count, st_h.data()},
+                      RB{c->n_iter, (int)sizeof(int) * count, it_h.data()},
+                      RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
+        const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
+        for (int b = 0; b < count; ++b)
+            if (st_h[b] == 0) c->slot_wide[hs[b]] = wide_h[b];
+    }
     for (int b = 0; b < count; ++b) {
         status[b] = st_h[b];
         if (nops) {
@@ -985,7 +999,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->lstride = 2 * c->nb;
     c->ldet = dalloc<double>(c, B * c->lstride);
     c->out = dalloc<double>(c, B);
-    c->pstride = (int64_t)(c->nb + 1) * c->sp;
+    c->pstride = (int64_t)c->nb * c->sp;
     c->partial = dalloc<double>(c, B * c->pstride);
     const int64_t vs = np;
     c->vecbase = dalloc<double>(c, 8 * B * vs);
@@ -1006,7 +1020,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 20, hipHostMallocDefault));
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 16,
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 20,
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, B);
@@ -1025,12 +1039,17 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
                        sizeof(double) * (size_t)B * std::max(c->P, 1), hipHostMallocDefault));
     c->U64 = dalloc<double>(c, n * S);
     const int64_t Lsz = (np + 64) * np;
-    c->Sl = SlotSet{dalloc<float>(c, n_slots * Lsz), dalloc<float>(c, n_slots * np),
-                    dalloc<float>(c, n_slots * np), dalloc<double>(c, n_slots * np),
-                    dalloc<double>(c, n_slots), Lsz, np};
+    c->Sl = SlotSet{dalloc<float>(c, n_slots * Lsz), dalloc<double>(c, n_slots * np),
+                    dalloc<double>(c, n_slots * np), dalloc<double>(c, n_slots * np),
+                    dalloc<double>(c, n_slots), Lsz, np,
+                    dalloc<double>(c, n_slots * np * np), dalloc<double>(c, n_slots * np),
+                    dalloc<int>(c, n_slots), dalloc<int>(c, B), np * np, APM_WIDE_Q};
+    if (const char* e = getenv("APM_WIDE_Q")) c->Sl.wide_q = atof(e);  // development knob
     HIPC(hipMemset(c->Sl.cst, 0, sizeof(double) * n_slots));
-    c->Up = UPool{dalloc<float>(c, n_ubufs * np * c->sp), np * c->sp, c->sp};
-    HIPC(hipMemset(c->Up.base, 0, sizeof(float) * n_ubufs * np * c->sp));
+    HIPC(hipMemset(c->Sl.wide, 0, sizeof(int) * n_slots));
+    c->slot_wide.assign((size_t)n_slots, 0);
+    c->Up = UPool{dalloc<double>(c, n_ubufs * np * c->sp), np * c->sp, c->sp};
+    HIPC(hipMemset(c->Up.base, 0, sizeof(double) * n_ubufs * np * c->sp));
 }
 
 void free_ctx(apm_ctx* c) {
@@ -1131,8 +1150,8 @@ int apm_u_download(apm_ctx* c, int64_t ubuf, double* U, int64_t ldu) {
         return fail(c, APM_E_INVALID, "apm_u_download: bad arguments");
     try {
         HIPC(hipSetDevice(c->device));
-        std::vector<float> h((size_t)c->np * c->sp);
-        HIPC(hipMemcpyAsync(h.data(), c->Up.base + ubuf * c->Up.stride, sizeof(float) * h.size(),
+        std::vector<double> h((size_t)c->np * c->sp);
+        HIPC(hipMemcpyAsync(h.data(), c->Up.base + ubuf * c->Up.stride, sizeof(double) * h.size(),
                             hipMemcpyDeviceToHost, c->stream));
         sync(c);
         for (int i = 0; i < c->n; ++i)
@@ -1245,8 +1264,7 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
         pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
         upload_h3(c, 1);
-        HIPC(hipMemcpyAsync(c->d_slots, &slot, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-        HIPC(hipMemcpyAsync(c->d_ubufs, &ubuf, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+        upload_idx(c, 1, &slot, &ubuf);  // (the pinned copy is the slot the read-back marks)
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);
     } catch (const HipError& e) {
         return fail(c, APM_E_HIP, e.msg);
@@ -1265,7 +1283,9 @@ int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* u
         HIPC(hipSetDevice(c->device));
         upload_idx(c, (int)count, slots, ubufs);
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
-        u_eval_device(c, (int)count);
+        bool wide = false;
+        for (int64_t b = 0; b < count; ++b) wide |= c->slot_wide[slots[b]] != 0;
+        u_eval_device(c, (int)count, wide);
         read_back(c, {RB{c->out, (int)sizeof(double) * (int)count, out_logf},
                       RB{c->status, (int)sizeof(int) * (int)count, status}});
     } catch (const HipError& e) {

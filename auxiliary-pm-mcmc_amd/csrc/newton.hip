@@ -277,12 +277,21 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     const double* Ab = A.base + b * A.cstride;
     float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
     const int64_t off = (mode == 0) ? np : 0;
+    double q = 0.0;  // squared norm of factor row r (the wide-slot test, k_slot_write_vec)
     if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
         const double* src = Ab + ((int64_t)np + r) * A.ld;
-        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? (float)src[np - 1 - c] : 0.0f;
+        for (int c = lane; c < np; c += 64) {
+            const double x = (c <= r) ? src[np - 1 - c] : 0.0;
+            L[c] = (float)x;
+            q += x * x;
+        }
     } else if (r < np) {
         const double* src = Ab + (off + r) * A.ld + off;
-        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? (float)src[c] : 0.0f;
+        for (int c = lane; c < np; c += 64) {
+            const double x = (c <= r) ? src[c] : 0.0;
+            L[c] = (float)x;
+            q += x * x;
+        }
     } else if (r == np && mode == 0) {
         const double* src = Ab + (2 * (int64_t)np) * A.ld + np;
         for (int c = lane; c < np; c += 64) L[c] = (float)src[c];
@@ -292,40 +301,70 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     } else {
         for (int c = lane; c < np; c += 64) L[c] = 0.0f;
     }
+    if (r < np) {
+        q = wave_sum_d(q);
+        if (lane == 0) S.rowq[slots[b] * S.vstride + r] = q;
+    }
 }
 
+// the fp64 factor of the call's wide slots (k_slot_write_vec decided), for k_ugemm64
+__global__ __launch_bounds__(256) void k_slot_write_L64(MatB A, SlotSet S,
+                                                        const int64_t* __restrict__ slots,
+                                                        int mode, int np, Live live) {
+    const int b = blockIdx.y;
+    if (live.status[b] != 0 || !S.wide[slots[b]]) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 4 + w;  // 0 .. np-1
+    const double* Ab = A.base + b * A.cstride;
+    double* L = S.L64 + slots[b] * S.l64stride + (int64_t)r * np;
+    const int64_t off = (mode == 0) ? np : 0;
+    if (mode == 2) {
+        const double* src = Ab + ((int64_t)np + r) * A.ld;
+        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? src[np - 1 - c] : 0.0;
+    } else {
+        const double* src = Ab + (off + r) * A.ld + off;
+        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? src[c] : 0.0;
+    }
+}
+
+// fp64 slot vectors of the self-consistent IS epilogue (ugemm.hip): f_post, W (last Newton
+// iteration, the one C is built with: latent_posterior_approximations.py:107-112) and
+// z = C^-1 f_post = K^-1 f_post + W f_post = a + W f_post (f_post = K a exactly, lpa.py:95), and
+// cst = 1/2 f_post^T z - 1/2 log|B| (= 1/2 |C_chol^-1 f_post|^2 - 1/2 log|B|); PriorMC: zeros.
 __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, const double* ldet,
                                                         int64_t lstride, int nb, SlotSet S,
                                                         const int64_t* __restrict__ slots,
                                                         int mode, int n, Live live) {
+    (void)A;
     const int b = blockIdx.x;
     if (live.status[b] != 0) return;
     __shared__ double red[4];
     const int64_t np = (int64_t)nb * 64;
     const int64_t so = slots[b] * S.vstride;
-    double gg = 0.0;
+    double fz = 0.0, tq = 0.0;
     for (int i = threadIdx.x; i < np; i += 256) {
+        tq += S.rowq[so + i];
         const bool is = (mode != 1) && i < n;
         const double f = is ? v.f[b * v.vstride + i] : 0.0;
         const double W = is ? v.W[b * v.vstride + i] : 0.0;
-        S.fpost[so + i] = (float)f;
+        const double z = is ? v.a[b * v.vstride + i] + W * f : 0.0;
         S.fpost64[so + i] = f;
-        S.W[so + i] = (float)W;
-        if (mode == 0) {
-            const double g = A.base[b * A.cstride + 2 * np * A.ld + np + i];
-            gg += g * g;
-        } else if (mode == 2) {
-            const double g = v.Kb[b * v.vstride + i];
-            gg += g * g;
-        }
+        S.W64[so + i] = W;
+        S.z64[so + i] = z;
+        fz += f * z;
     }
-    gg = block_sum_d(gg, red);
+    fz = block_sum_d(fz, red);
+    __syncthreads();
+    tq = block_sum_d(tq, red);
     if (threadIdx.x == 0) {
+        const int wd = tq > S.wide_q ? 1 : 0;
+        S.wide[slots[b]] = wd;
+        S.chain_wide[b] = wd;
         double c = 0.0;
         if (mode != 1) {
             double ld = 0.0;
             for (int k = 0; k < nb; ++k) ld += ldet[b * lstride + k];
-            c = -0.5 * gg - ld;
+            c = 0.5 * fz - ld;
         }
         S.cst[slots[b]] = c;
     }
@@ -338,6 +377,8 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
                        mode, np, v.Kb, v.vstride, live);
     hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
+    hipLaunchKernelGGL(k_slot_write_L64, dim3(np / 4, nchains), dim3(256), 0, s, A, S, slots, mode,
+                       np, live);
 }
 
 // Per-call read-back of small per-chain arrays (Newton flags, refinement mask, estimates,
@@ -349,7 +390,7 @@ __global__ __launch_bounds__(256) void k_export(Export e) {
     const int t = blockIdx.x * 256 + threadIdx.x;
     int off = 0;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         if (t >= off && t < off + e.words[k]) e.dst[t] = e.src[k][t - off];
         off += e.words[k];
     }
@@ -357,7 +398,7 @@ __global__ __launch_bounds__(256) void k_export(Export e) {
 }
 
 void launch_export(const Export& e, hipStream_t s) {
-    const int tot = e.words[0] + e.words[1] + e.words[2];
+    const int tot = e.words[0] + e.words[1] + e.words[2] + e.words[3];
     if (tot <= 0) return;
     hipLaunchKernelGGL(k_export, dim3((tot + 255) / 256), dim3(256), 0, s, e);
 }

@@ -1,21 +1,25 @@
 // Importance-sampling u-path: f_s = f_post + L U (fp32 MFMA), probit epilogue, log-mean-exp.
 //
 // Replaces gpdemo/estimators.py:221-241 (ApproxPosteriorIS, theta- and cached u-calls) and
-// :323-325 (PriorMC) in the algebraically identical form of DESIGN.md §3:
-//   log w_s = sum_n [log Phi(y_n f_sn) + 1/2 W_n f_sn^2] - g^T u_s + cst,
-//   cst = -1/2 |g|^2 - 1/2 log|B|          (IS);     W = 0, g = 0, cst = 0   (PriorMC)
-// g^T u_s comes out of the same GEMM: g^T is stored as row np of the slot's factor, so the extra
-// 64-row block of the output holds it in its first row.
+// :323-325 (PriorMC) in the algebraically identical, self-consistent form of DESIGN.md §3.2:
+//   log w_s = sum_n [log Phi(y_n f_sn) + 1/2 W_n f_sn^2 - z_n f_sn] + cst,
+//   z = C^-1 f_post = a + W f_post,  cst = 1/2 f_post^T z - 1/2 log|B|   (IS)
+//   W = 0, z = 0, cst = 0                                               (PriorMC)
+// i.e. the reference's log p(y|f) + log p(f) - log q(f) evaluated AT the computed f_s (with
+// K^-1 = C^-1 - W and |C|/|K| = 1/|B|): no term uses u_s itself, so the fp32 rounding of L, U and
+// the MFMA accumulation moves f_s but not the consistency of the three terms, whose sum has a
+// vanishing gradient in f_s at the Laplace mode - as in the reference's own evaluation. The large
+// terms (1/2 W f^2, z f, the -x^2/2 of log Phi) are formed and summed in fp64.
 #include "apm_internal.h"
 
 // ------------------------------------------------------------------------------- U buffers
 __global__ __launch_bounds__(256) void k_u_convert(const double* __restrict__ U, int64_t ldu,
-                                                   int n, int S, float* __restrict__ dst, int sp,
+                                                   int n, int S, double* __restrict__ dst, int sp,
                                                    int np) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= (int64_t)np * sp) return;
     const int r = (int)(e / sp), c = (int)(e % sp);
-    dst[e] = (r < n && c < S) ? (float)U[(int64_t)r * ldu + c] : 0.0f;
+    dst[e] = (r < n && c < S) ? U[(int64_t)r * ldu + c] : 0.0;
 }
 
 void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int64_t ubuf,
@@ -80,11 +84,11 @@ __global__ __launch_bounds__(256) void k_u_normal(UPool P, const int64_t* __rest
         z[2 * h] = rr * cs;
         z[2 * h + 1] = rr * sn;
     }
-    float* dst = P.base + ubufs[b] * P.stride;
+    double* dst = P.base + ubufs[b] * P.stride;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
         const int64_t e = q * 4 + h;
-        if (e < tot) dst[(e / S) * P.sp + (e % S)] = z[h];
+        if (e < tot) dst[(e / S) * P.sp + (e % S)] = (double)z[h];
     }
 }
 
@@ -103,8 +107,8 @@ __global__ __launch_bounds__(256) void k_u_combine(UPool P, const int64_t* __res
     const int b = blockIdx.y;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= tot) return;
-    const float x = P.base[a[b] * P.stride + e], v = P.base[bb[b] * P.stride + e];
-    P.base[dst[b] * P.stride + e] = (float)ca[b] * x + (float)cb[b] * v;
+    const double x = P.base[a[b] * P.stride + e], v = P.base[bb[b] * P.stride + e];
+    P.base[dst[b] * P.stride + e] = ca[b] * x + cb[b] * v;
 }
 
 void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64_t* b,
@@ -122,6 +126,11 @@ void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64
 // C/D lane l, reg r -> (row = (l>>4)*4 + r, col = l&15)
 #define UP 65  // LDS row pitch (floats) of the staged U tile: conflict-free B-fragment reads
 
+// one entry of the per-sample sum: log Phi(y f) + 1/2 W f^2 - z f, the large terms in fp64
+__device__ __forceinline__ double is_term(double f, double y, double W, double z) {
+    return log_ndtr_mixed(y * f) + (0.5 * W * f - z) * f;
+}
+
 __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restrict__ slots,
                                                UPool P, const int64_t* __restrict__ ubufs,
                                                const double* __restrict__ y, int n, int np,
@@ -135,14 +144,14 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     // workgroups that share row block i's slice of L run together on one XCD and read it once
     // from its L2, and a chain's U stays within one XCD's L2 / the Infinity Cache.
     const int nb = np / 64;
-    const long total = (long)(nb + 1) * nsb * nchains;
+    const long total = (long)nb * nsb * nchains;
     const long slot_id = blockIdx.x, xcd = slot_id & 7, q = total >> 3, rem = total & 7;
     const long item = nchains < 8 ? slot_id  // too few chains to fill 8 XCDs evenly: plain order
                       : (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (slot_id >> 3);
-    const int b = (int)(item / ((long)(nb + 1) * nsb));
-    const int rest = (int)(item % ((long)(nb + 1) * nsb));
+    const int b = (int)(item / ((long)nb * nsb));
+    const int rest = (int)(item % ((long)nb * nsb));
     if (status[b] != 0) return;
-    const int i = nb - rest / nsb;
+    const int i = nb - 1 - rest / nsb;
     const int sb = rest % nsb;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
     const int r16 = lane & 15, kq = lane >> 4;
@@ -150,10 +159,11 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     __shared__ double csum[2][64];
 
     const int64_t slot = slots[b];
+    if (S.wide[slot]) return;  // k_ugemm64
     const float* L = S.L + slot * S.lstride;
-    const float* U = P.base + ubufs[b] * P.stride;
+    const double* U = P.base + ubufs[b] * P.stride;
     const int sp = P.sp;
-    const int kend = (i == nb) ? np : (i + 1) * 64;
+    const int kend = (i + 1) * 64;
 
     f4_t acc[2][2];
 #pragma unroll
@@ -169,9 +179,11 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     auto gload = [&](int kk) {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
-            const int e = tid + h * 256;  // float4 index 0..1023
-            un[h] = *reinterpret_cast<const f4_t*>(U + (int64_t)(kk + (e >> 4)) * sp + sb * 64 +
-                                                   (e & 15) * 4);
+            const int e = tid + h * 256;  // 4-element piece 0..1023
+            const double* pu = U + (int64_t)(kk + (e >> 4)) * sp + sb * 64 + (e & 15) * 4;
+            const d2_t u0 = *reinterpret_cast<const d2_t*>(pu);
+            const d2_t u1 = *reinterpret_cast<const d2_t*>(pu + 2);
+            un[h] = f4_t{(float)u0[0], (float)u0[1], (float)u1[0], (float)u1[1]};
         }
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
@@ -213,32 +225,98 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     }
 
     double* pb = partial + b * pstride;
-    if (i == nb) {
-        // g^T u_s sits in output row np = first row of this block: wr=0, bi=0, lane>>4=0, r=0
-        if (wr == 0 && kq == 0) {
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj)
-                pb[(int64_t)nb * sp + sb * 64 + 32 * wc + 16 * bj + r16] = (double)acc[0][bj][0];
-        }
-        return;
-    }
-    const float* fp = S.fpost + slot * S.vstride;
-    const float* Wv = S.W + slot * S.vstride;
+    const double* fp = S.fpost64 + slot * S.vstride;
+    const double* Wv = S.W64 + slot * S.vstride;
+    const double* zv = S.z64 + slot * S.vstride;
     double colsum[2];
 #pragma unroll
     for (int bj = 0; bj < 2; ++bj) {
-        float s = 0.f;
+        double d = 0.0;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = i * 64 + 32 * wr + 16 * bi + kq * 4 + r;
-                if (row < n) {
-                    const float f = fp[row] + acc[bi][bj][r];
-                    s += log_ndtr_f((float)y[row] * f) + 0.5f * Wv[row] * f * f;
-                }
+                if (row < n) d += is_term(fp[row] + (double)acc[bi][bj][r], y[row], Wv[row], zv[row]);
             }
-        double d = (double)s;
+        d += __shfl_xor(d, 16, 64);
+        d += __shfl_xor(d, 32, 64);
+        colsum[bj] = d;
+    }
+    if (kq == 0) {
+        csum[wr][32 * wc + r16] = colsum[0];
+        csum[wr][32 * wc + 16 + r16] = colsum[1];
+    }
+    __syncthreads();
+    if (tid < 64) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
+}
+
+// The same product and epilogue on f64 MFMA (v_mfma_f64_16x16x4_f64) for the call's WIDE slots
+// (S.wide: trace(L L^T) > APM_WIDE_Q, set by k_slot_write_vec), from the slot's fp64 factor and
+// the fp64 U buffer: where the entries of f_s are large (sigma = e^18.5: |f_s| ~ 1e4), the fp32
+// rounding of L and U alone moves log f by ~10 nats. Rare (extreme theta),
+// so plainly staged: 64x64 output tile per workgroup, L and U slices of 16 through LDS.
+__global__ __launch_bounds__(256) void k_ugemm64(SlotSet S, const int64_t* __restrict__ slots,
+                                                 UPool P, const int64_t* __restrict__ ubufs,
+                                                 const double* __restrict__ y, int n, int np,
+                                                 double* __restrict__ partial, int64_t pstride,
+                                                 const int* __restrict__ status, int nsb) {
+    const int nb = np / 64;
+    const int b = blockIdx.y;
+    if (status[b] != 0) return;
+    const int64_t slot = slots[b];
+    if (!S.wide[slot]) return;
+    const int i = (int)blockIdx.x / nsb, sb = (int)blockIdx.x % nsb;
+    (void)nb;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    __shared__ double La[64][17];
+    __shared__ double Ub[16][65];
+    __shared__ double csum[2][64];
+    const double* L = S.L64 + slot * S.l64stride;
+    const double* U = P.base + ubufs[b] * P.stride;
+    const int sp = P.sp;
+    d4_t acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4_t{0.0, 0.0, 0.0, 0.0};
+    const int kend = (i + 1) * 64;
+    for (int kk = 0; kk < kend; kk += 16) {
+        for (int e = tid; e < 64 * 16; e += 256) {
+            const int r = e >> 4, c = e & 15;
+            La[r][c] = L[(int64_t)(i * 64 + r) * np + kk + c];
+            Ub[e >> 6][e & 63] = U[(int64_t)(kk + (e >> 6)) * sp + sb * 64 + (e & 63)];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                        La[32 * wr + 16 * bi + r16][4 * t + kq],
+                        Ub[4 * t + kq][32 * wc + 16 * bj + r16], acc[bi][bj], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // f64 MFMA output map: lane l, reg r -> row (l >> 4) + 4r, col l & 15
+    double* pb = partial + b * pstride;
+    const double* fp = S.fpost64 + slot * S.vstride;
+    const double* Wv = S.W64 + slot * S.vstride;
+    const double* zv = S.z64 + slot * S.vstride;
+    double colsum[2];
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) {
+        double d = 0.0;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = i * 64 + 32 * wr + 16 * bi + kq + 4 * r;
+                if (row < n) d += is_term(fp[row] + acc[bi][bj][r], y[row], Wv[row], zv[row]);
+            }
         d += __shfl_xor(d, 16, 64);
         d += __shfl_xor(d, 32, 64);
         colsum[bj] = d;
@@ -253,11 +331,14 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
 
 void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
                   const double* y, int n, int np, double* partial, int64_t pstride,
-                  const int* status, int nchains, hipStream_t s) {
+                  const int* status, int nchains, bool wide, hipStream_t s) {
     const int nb = np / 64, nsb = P.sp / 64;
-    const long total = (long)(nb + 1) * nsb * nchains;
+    const long total = (long)nb * nsb * nchains;
     hipLaunchKernelGGL(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
                        np, partial, pstride, status, nsb, nchains);
+    if (wide)
+        hipLaunchKernelGGL(k_ugemm64, dim3((unsigned)(nb * nsb), nchains), dim3(256), 0, s, S,
+                           slots, P, ubufs, y, n, np, partial, pstride, status, nsb);
 }
 
 // logsumexp_s(lw_s) - log S per chain
@@ -274,7 +355,7 @@ __global__ __launch_bounds__(256) void k_lme(const double* __restrict__ partial,
     const double cst = Sl.cst[slots[b]];
     double mx = -INFINITY;
     for (int s = threadIdx.x; s < S; s += 256) {
-        double v = cst - pb[(int64_t)nb * sp + s];
+        double v = cst;
         for (int i = 0; i < nb; ++i) v += pb[(int64_t)i * sp + s];
         if (s < 1024) lw[s] = v;
         mx = fmax(mx, v);
@@ -287,7 +368,7 @@ __global__ __launch_bounds__(256) void k_lme(const double* __restrict__ partial,
         if (s < 1024) {
             v = lw[s];
         } else {
-            v = cst - pb[(int64_t)nb * sp + s];
+            v = cst;
             for (int i = 0; i < nb; ++i) v += pb[(int64_t)i * sp + s];
         }
         se += exp(v - mx);

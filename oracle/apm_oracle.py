@@ -237,7 +237,7 @@ def theta_state_reformulated(K, y):
     g = la.solve_triangular(C_chol, f_post, lower=True)
     logdet_B = 2. * np.log(st['L'].diagonal()).sum()
     return dict(C_chol=C_chol, f_post=f_post, W=st['W_diag'], g=g, logdet_B=logdet_B,
-                n_ops=n_ops)
+                n_ops=n_ops, a=st['a'])
 
 
 def theta_state_pushthrough(K, y):
@@ -257,7 +257,8 @@ def theta_state_pushthrough(K, y):
     C_chol = la.solve_triangular(U, K_chol.T, lower=False).T   # (U^-1 L_K^T)^T = L_K U^-T
     g = la.solve_triangular(C_chol, f_post, lower=True)
     logdet_M = 2. * np.log(Lp.diagonal()).sum()
-    return dict(C_chol=C_chol, f_post=f_post, W=W, g=g, logdet_B=logdet_M, n_ops=n_ops)
+    return dict(C_chol=C_chol, f_post=f_post, W=W, g=g, logdet_B=logdet_M, n_ops=n_ops,
+                a=st['a'])
 
 
 def is_estimate_reformulated(y, state, ns):
@@ -266,6 +267,23 @@ def is_estimate_reformulated(y, state, ns):
     t = log_ndtr(y[:, None] * f_s) + 0.5 * state['W'][:, None] * f_s ** 2
     g = state['g']
     lw = t.sum(0) - g.dot(ns) - 0.5 * g.dot(g) - 0.5 * state['logdet_B']
+    return logsumexp(lw) - np.log(ns.shape[1])
+
+
+def is_estimate_consistent(y, state, ns, C_chol=None):
+    """The device's self-consistent form of estimators.py:221-241 (ugemm.hip):
+    the reference's log p(y|f) + log p(f) - log q(f) evaluated at f_s = f_post + C_chol u_s with
+    K^-1 = C^-1 - W and |C| / |K| = 1 / |B| substituted and the quadratic forms expanded around
+    f_post, so that nothing but f_s enters per sample:
+      log w_s = sum_n [log Phi(y_n f_sn) + 1/2 W_n f_sn^2 - z_n f_sn] + 1/2 f_post^T z
+                - 1/2 log|B|,   z = C^-1 f_post = a + W f_post  (f_post = K a, lpa.py:95).
+    C_chol: the factor to form f_s with (default: the state's; the GPU passes its fp32 one)."""
+    L = state['C_chol'] if C_chol is None else C_chol
+    f_post, W = state['f_post'], state['W']
+    z = state['a'] + W * f_post
+    f_s = f_post[:, None] + L.dot(ns)                                  # (N, S)
+    t = log_ndtr(y[:, None] * f_s) + (0.5 * W[:, None] * f_s - z[:, None]) * f_s
+    lw = t.sum(0) + 0.5 * f_post.dot(z) - 0.5 * state['logdet_B']
     return logsumexp(lw) - np.log(ns.shape[1])
 
 

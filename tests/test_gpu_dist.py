@@ -62,5 +62,5 @@ def test_config3_rank_shares_consistent(gpu_available):
         U = smp.ctx.u_download(smp.ub_u[c])
         v, _, _ = orc.is_estimate(X, y, kf, U, smp.theta[c])
         lp = smp.log_prior(smp.theta[c][None])[0]
-        assert abs(smp.log_f[c] - (v + lp)) <= 1e-3 + 2e-7 * abs(v), (rank, smp.log_f[c], v + lp)
+        assert abs(smp.log_f[c] - (v + lp)) <= 5e-4, (rank, smp.log_f[c], v + lp)
         smp.ctx.close()

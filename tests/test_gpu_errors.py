@@ -70,7 +70,7 @@ def test_chol_k_failure_raises_linalgerror(nat):
     # the estimator is still usable after the failure
     v, _ = es(ns, np.array([0.3, 0.4]))
     r, _, _ = orc.is_estimate(X, y, orc.make_kernel_func('iso', 1e-8), ns, np.array([0.3, 0.4]))
-    assert abs(v - r) <= 1e-3
+    assert abs(v - r) <= 5e-4
 
 
 def test_failing_chain_masked_in_batch(nat):
@@ -128,4 +128,4 @@ def test_invalid_covariance_deviation_pinned(nat, name):
     st = orc.theta_state_pushthrough(K, y)
     r = orc.is_estimate_reformulated(y, st, ns)
     assert np.isfinite(v)
-    assert abs(v - r) <= 1e-3 + 1e-6 * abs(r), (v, r)
+    assert abs(v - r) <= 5e-4, (v, r)

@@ -2,7 +2,7 @@
 the golden vectors produced by the reference (tests/golden/make_golden.py).
 
 Tolerances (DESIGN.md §5): theta-path quantities are fp64 (Gram 1e-13 rel; Laplace f 1e-9 rel);
-estimator values go through the fp32 MFMA L.U and are checked to |d log f| <= 2e-3 + 2e-5 |log f|.
+estimator values go through the fp32 MFMA L.U and are checked to |d log f| <= 5e-4 nats.
 """
 import numpy as np
 import pytest
@@ -12,7 +12,7 @@ from conftest import golden
 
 pytestmark = pytest.mark.gpu
 
-TOL_ABS, TOL_REL = 2e-3, 2e-5
+TOL_ABS, TOL_REL = 5e-4, 0.0  # nats; no relative term
 
 
 def _close(v, ref):

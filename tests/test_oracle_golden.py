@@ -90,6 +90,24 @@ def test_reformulated_is_equals_reference_form():
             assert abs(v - ref) < 1e-7 * max(1., abs(ref)), (ci, v, ref)
 
 
+def test_consistent_is_equals_reference_form():
+    """The self-consistent form the device evaluates (ugemm.hip: nothing but f_s per sample,
+    z = a + W f_post = C^-1 f_post) equals the reference's estimates on its own outputs, and -
+    unlike the u-expanded form - it is insensitive to a perturbation of f_s's factor: with C_chol
+    rounded to fp32 (the slot's precision) it moves by far less than the u-expanded form does."""
+    for ci, c in _cases():
+        st = orc.theta_state_reformulated(c['K'], c['y'])
+        L32 = st['C_chol'].astype(np.float32).astype(np.float64)
+        for ns, key in ((c['ns1'], 'is_logf1'), (c['ns2'], 'is_logf2')):
+            ref = float(c[key])
+            v = orc.is_estimate_consistent(c['y'], st, ns)
+            assert abs(v - ref) < 1e-7 * max(1., abs(ref)), (ci, v, ref)
+            d_cons = abs(orc.is_estimate_consistent(c['y'], st, ns, L32) - ref)
+            st32 = dict(st, C_chol=L32)
+            d_exp = abs(orc.is_estimate_reformulated(c['y'], st32, ns) - ref)
+            assert d_cons <= max(d_exp, 1e-9), (ci, d_cons, d_exp)
+
+
 def test_laplace_max_iters_error():
     e = golden('errors')
     with pytest.raises(orc.MaximumIterationsExceededError) as ei:
