@@ -198,6 +198,23 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s);
 
+// ---- ozaki.hip: fp64 trailing updates emulated exactly on int8 MFMA ---------------------------
+#define OZ_NM 15  // moduli (pairwise coprime, <= 256; log2 of their product 118.57)
+struct OzPlanes {
+    int8_t* base;     // per chain: OZ_NM planes of rows x depth int8 residues
+    int64_t mstride;  // bytes per plane (rows * depth)
+    int64_t cstride;  // bytes per chain
+    int* exps;        // per chain: row scale exponents (row r - row0)
+    int64_t estride;
+    int row0;         // matrix row of plane row 0
+};
+hipError_t oz_init_device();
+int oz_beta(int depth);
+void launch_oz_split(MatB A, int row0, int nrows, int col0, int depth, OzPlanes P, int beta,
+                     Live live, int nchains, hipStream_t s);
+void launch_oz_update_t128(MatB A, OzPlanes P, int depth, const unsigned* tiles, int ntiles,
+                           int plus, Live live, int nchains, hipStream_t s, FusedDiag<double> fd);
+
 // ---- postcov.hip ----------------------------------------------------------------------------
 void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,
                     Live live, int nchains, hipStream_t s);

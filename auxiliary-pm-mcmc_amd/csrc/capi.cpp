@@ -90,6 +90,11 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
     bool gram2 = true;    // APM_GRAM2=0: K's working copies by k_copy_lower instead of the Gram
+    // fp64 outer (rank-64*OUTER) trailing updates on int8 MFMA (ozaki.hip, APM_OZAKI); one
+    // residue-plane buffer per stream (the concurrent chol(K) runs on stream2)
+    bool ozaki = false;
+    OzPlanes ozp[2]{};
+    int64_t oz_rows = 0;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     int t128 = 3;
     bool left_inner = true;
@@ -268,7 +273,20 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
     if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         const auto sl = super_list(c, i0, R, j0, jend, g);
-        launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd);
+        if (c->ozaki && plus != 2 && kc <= OUTER && kc % 4 == 0 &&
+            (int64_t)(R - j0) * 64 <= c->oz_rows) {
+            // rows [j0, R) of the panel's columns -> residue planes, then the int8 update
+            OzPlanes P = c->ozp[E.s == c->stream2 ? 1 : 0];
+            P.row0 = j0 * 64;
+            const int depth = 64 * kc;
+            P.mstride = c->oz_rows * depth;
+            launch_oz_split(M, j0 * 64, (R - j0) * 64, k0 * 64, depth, P, oz_beta(depth), E.lv,
+                            count, E.s);
+            check_launch();
+            launch_oz_update_t128(M, P, depth, sl.first, sl.second, plus, E.lv, count, E.s, fd);
+        } else {
+            launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd);
+        }
     } else {
         if (plus == 2) throw HipError{"identity-initialised update needs the t128 path"};
         launch_chol_update(M, k0, kc, tl.first, tl.second, plus != 0, E.lv, count, E.s, fd);
@@ -949,6 +967,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_GRAM2")) c->gram2 = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
+    if (const char* e = getenv("APM_OZAKI")) c->ozaki = atoi(e) != 0;
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_MW")) c->trsv_mw = atoi(e) != 0;
@@ -1024,6 +1043,18 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, B);
+    if (c->ozaki) {  // residue planes for rows of the largest factorisation (2 np + 64)
+        HIPC(oz_init_device());
+        c->oz_rows = 2 * np + 64;
+        for (int q = 0; q < 2; ++q) {
+            OzPlanes& P = c->ozp[q];
+            P.mstride = c->oz_rows * 64 * OUTER;
+            P.cstride = (int64_t)OZ_NM * P.mstride;
+            P.base = dalloc<int8_t>(c, (size_t)B * P.cstride);
+            P.estride = c->oz_rows;
+            P.exps = dalloc<int>(c, (size_t)B * c->oz_rows);
+        }
+    }
     // + 1: the count of bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS)
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 1);
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 1)));
