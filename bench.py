@@ -483,6 +483,31 @@ def ess_block(dist, smp, series, done, burn, elapsed, P):
                           'gelman.diag restatement, max over components (and ranks)'.format(P)}}
 
 
+def ess_long_record(value, a):
+    """The long-chain ESS record of this workload (SURVEY.md §8d protocol: 500 warm-up
+    transitions discarded, 2000 kept per chain; tools/ess_long.py on one MI355X -> the newest
+    profiles/r*_ess_long.json): its ESS per transition (min over the theta components) x this
+    run's transitions/s. The in-run ess_per_sec above rests on 100-transition segments, where the
+    AR fit cannot see the slow modes of a 33-dimensional random-direction slice sampler, and
+    over-states the long-chain figure ~4x."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_ess_long.json')))
+    if not files:
+        return None
+    r = json.load(open(files[-1]))
+    cfg = r.get('config', {})
+    if (cfg.get('n_data'), cfg.get('n_features'), cfg.get('n_imp')) != (a.n, a.d, a.n_imp):
+        return None
+    ept = r['ess_per_transition_min_component']
+    return {'source': os.path.relpath(files[-1], REPO),
+            'ess_per_transition_min_component': ept,
+            'ess_per_sec_estimate': ept * value,
+            'rhat_max': r['rhat_max'], 'chains': cfg.get('chains'),
+            'warmup_discarded': cfg.get('warmup_discarded'),
+            'kept_per_chain': cfg.get('kept_per_chain'),
+            'note': 'ESS per transition from the long-chain record x this run\'s transitions/s'}
+
+
 def main():
     a = parse()
     dist = Dist()
@@ -710,6 +735,7 @@ def main():
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)
+    line['ess_long_chain'] = ess_long_record(value, a)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     ok = parity is None or parity['pass']
