@@ -198,6 +198,8 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s);
 
+extern bool H3DMA;  // chol32.hip: LDS-DMA staging for the fp16x3 trailing update (APM_H3DMA)
+
 // ---- ozaki.hip: fp64 trailing updates emulated exactly on int8 MFMA ---------------------------
 #define OZ_NM 15  // moduli (pairwise coprime, <= 256; log2 of their product 118.57)
 struct OzPlanes {

@@ -968,6 +968,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_OZAKI")) c->ozaki = atoi(e) != 0;
+    {  // process-wide kernel choice, re-read at every context creation (default: off)
+        const char* e = getenv("APM_H3DMA");
+        H3DMA = e ? atoi(e) != 0 : false;
+    }
     if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
     if (const char* e = getenv("APM_TRSV_MW")) c->trsv_mw = atoi(e) != 0;

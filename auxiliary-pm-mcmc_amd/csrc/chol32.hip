@@ -672,7 +672,11 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
         }
     }
 }
-template <bool H3>
+// DMA (with H3): the fp32 operands are staged by LDS-DMA as on the fp32 path and each wave splits
+// the fragments it reads into hi/lo in registers right before its MFMAs (the same split, the same
+// products in the same order: bitwise equal to the register-staged split) - no staging registers,
+// no ds_write pass of four half planes, and the split's VALU work interleaves with the MFMAs.
+template <bool H3, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
@@ -726,7 +730,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
             for (int r = 0; r < 4; ++r)
                 acc[bi][bj][r] = -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
     // super-tile rows below hlim (the appended right-hand side row), chains flagged in h3ok
-    if (H3 && ti + (rv1 ? 1 : 0) < hlim && (!h3ok || h3ok[b])) {
+    const bool use_h3 = H3 && ti + (rv1 ? 1 : 0) < hlim && (!h3ok || h3ok[b]);
+    if (!DMA && use_h3) {
         // register staging: thread tid moves 16-byte pieces p = tid + 256h (row p/8, k 4(p%8))
         // of both operands
         const float* arow[4];
@@ -840,6 +845,42 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                                                  (lds_void_t*)&sm.g.b[buf][32 * wv + 8 * q][0], 16, 0, 0);
             }
         };
+        // fp16x3 from the fp32 image: lane (r16, kq) reads pieces 2kq, 2kq+1 (k = 8kq .. 8kq+7,
+        // the v_mfma_f32_16x16x32_f16 fragment) of its rows and splits them in registers
+        auto split8 = [](const f4_t& p0, const f4_t& p1, h8_t& hi, h8_t& lo) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float v = e < 4 ? p0[e] : p1[e - 4];
+                const _Float16 x = (_Float16)v;
+                hi[e] = x;
+                lo[e] = (_Float16)(v - (float)x);
+            }
+        };
+        auto compute_h3 = [&](int cur) {
+            const int s0 = ((2 * kq) ^ (r16 & 7)) * 4, s1 = ((2 * kq + 1) ^ (r16 & 7)) * 4;
+            h8_t bh[4], bl[4];
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj) {
+                const float* rowp = &sm.g.b[cur][64 * wc + 16 * bj + r16][0];
+                split8(*reinterpret_cast<const f4_t*>(rowp + s0),
+                       *reinterpret_cast<const f4_t*>(rowp + s1), bh[bj], bl[bj]);
+            }
+            h8_t ah[4], al[4];
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi) {
+                const float* rowp = &sm.g.a[cur][64 * wr + 16 * bi + r16][0];
+                split8(*reinterpret_cast<const f4_t*>(rowp + s0),
+                       *reinterpret_cast<const f4_t*>(rowp + s1), ah[bi], al[bi]);
+            }
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 4; ++bj) {
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                }
+        };
         // lane group kq takes the slice's k values 8kq .. 8kq+7 (pieces 2kq, 2kq+1; the same k for A
         // and B): a lane's fragments for 4 MFMA steps are one 16-byte LDS read
         auto compute = [&](int cur) {
@@ -866,11 +907,20 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         glds(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        for (int s = 0; s < nsub; ++s) {
-            if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
-            if (mine) compute(s & 1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+        if (DMA && use_h3) {  // (uniform per workgroup: one loop per operand precision)
+            for (int s = 0; s < nsub; ++s) {
+                if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);
+                if (mine) compute_h3(s & 1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
+        } else {
+            for (int s = 0; s < nsub; ++s) {
+                if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
+                if (mine) compute(s & 1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
         }
     }
 #pragma unroll
@@ -916,12 +966,18 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                       tid, 256);
 }
 
+// the LDS-DMA fp16x3 update (APM_H3DMA=1; bitwise equal, measured no faster in situ - DESIGN.md §5)
+bool H3DMA = false;
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
                                int hlim, const int* h3ok, int rhs) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    if (hlim > 0)
+    if (hlim > 0 && H3DMA)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_chol_update32_t128<true, true>), dim3((unsigned)total),
+                           dim3(256), 0, s, A, k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok,
+                           rhs);
+    else if (hlim > 0)
         hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
                            k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs);
     else

@@ -153,6 +153,41 @@ def device_sync():
         pass
 
 
+def csrc_sha16():
+    """Digest of the HIP/C++ sources of libapm.so (auxiliary-pm-mcmc_amd/csrc, include/apm.h):
+    binds a committed PMC profile to the build it was taken of (tools/profile_round.sh)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(REPO, 'auxiliary-pm-mcmc_amd', 'csrc', '*'))) + \
+        [os.path.join(REPO, 'include', 'apm.h')]
+    for f in files:
+        if f.endswith(('.hip', '.cpp', '.h')):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, 'rb').read())
+    return h.hexdigest()[:16]
+
+
+def _pmc_file():
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d, os.path.relpath(files[-1], REPO)
+
+
+def pmc_provenance():
+    """{source, csrc_sha16 of the profiled build, of this build, stale} for the PMC numbers."""
+    d, src = _pmc_file()
+    if d is None:
+        return None
+    prof = d.get('csrc_sha16')
+    cur = csrc_sha16()
+    return {'source': src, 'profiled_csrc_sha16': prof, 'commit': d.get('commit'),
+            'this_csrc_sha16': cur, 'stale': prof != cur}
+
+
 def pmc_traffic(*kernels):
     """HBM bytes per dispatch of the kernels (dispatch-weighted over the names given: the bench's
     HIP-event timing of a roofline covers all launch variants of one operation) inside the timed
@@ -160,11 +195,10 @@ def pmc_traffic(*kernels):
     written by tools/prof_window.py from separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc
     WRITE_SIZE` runs of the same command, with the guide's gfx950 corrections). PMC counters
     cannot be read live inside this process."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
-    if not files:
+    d, src = _pmc_file()
+    if d is None:
         return None, None
-    d = json.load(open(files[-1])).get('pmc_traffic', {})
+    d = d.get('pmc_traffic', {})
     tot = n = 0
     for k in kernels:
         e = d.get(k, {})
@@ -175,7 +209,7 @@ def pmc_traffic(*kernels):
             n += cnt
     if not n:
         return None, None
-    return tot / n, os.path.relpath(files[-1], REPO)
+    return tot / n, src
 
 
 # flops one MFMA busy cycle of one SIMD performs (MI355X_MICROARCH.md: v_mfma_f64_16x16x4_f64 at
@@ -190,11 +224,10 @@ def pmc_mfma(kind, *kernels):
     committed PMC pass of this bench (profiles/r*_pmc_traffic.json 'pmc_mfma', written by
     tools/prof_window.py). Counter runs serialise dispatches, so the utilisation is the kernel's
     own, without the concurrent chol(K) stream."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_traffic.json')))
-    if not files:
+    d, src = _pmc_file()
+    if d is None:
         return None
-    d = json.load(open(files[-1])).get('pmc_mfma', {})
+    d = d.get('pmc_mfma', {})
     busy = act = n = 0.0
     for k in kernels:
         e = d.get(k)
@@ -206,7 +239,7 @@ def pmc_mfma(kind, *kernels):
         return None
     return {'util': busy / (1024.0 * act / 8.0), 'dispatches': int(n),
             'counter_flops_per_launch': busy / n * MFMA_FLOPS_PER_BUSY_CYCLE[kind],
-            'source': os.path.relpath(files[-1], REPO)}
+            'source': src}
 
 
 def timed_region(dist, step_fn, steps, on_start=None):
@@ -735,6 +768,8 @@ def main():
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)
+    # the PMC numbers (traffic, mfma_busy) come from a committed counter pass: of this build?
+    line['pmc_provenance'] = pmc_provenance()
     line['ess_long_chain'] = ess_long_record(value, a)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)

@@ -286,6 +286,23 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
         assert ob1[b] == o1[b]
 
 
+def test_fp16x3_dma_staging_bitwise_equal(nat, monkeypatch):
+    """The LDS-DMA fp16x3 update (APM_H3DMA=1: fp32 operands staged as on the fp32 path, split
+    into hi/lo in registers before the MFMAs) against the register-staged split (default): the same
+    split and the same products in the same order, so the results are bitwise equal - including
+    a theta_0 >= 19 chain on fp32 operands in the same call."""
+    X, y, thetas, ns = _mixed_case()
+    th = thetas.copy()
+    th[2, 0] = 19.5
+    o0, s0, n0, f0 = _run_is(nat, X, y, th, ns, monkeypatch)
+    o1, s1, n1, f1 = _run_is(nat, X, y, th, ns, monkeypatch, APM_H3DMA=1)
+    np.testing.assert_array_equal(s1, s0)
+    np.testing.assert_array_equal(n1, n0)
+    for b in range(len(th)):
+        np.testing.assert_array_equal(f1[b], f0[b])
+        assert o1[b] == o0[b] or (np.isnan(o1[b]) and np.isnan(o0[b])), (b, o1[b], o0[b])
+
+
 def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
     """The Newton solves' 4-workgroup TRSV (k_trsv32_mw, default) against the one-workgroup
     kernel (APM_TRSV_MW=0): modes to 1e-9 relative (summation order only, amplified by the Newton

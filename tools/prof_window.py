@@ -48,6 +48,8 @@ def main():
     ap.add_argument('--write')
     ap.add_argument('--mfma')
     ap.add_argument('--out')
+    ap.add_argument('--csrc-sha16', help='bench.csrc_sha16() of the profiled build')
+    ap.add_argument('--commit', help='git describe of the profiled tree (build container)')
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     win = window(rows, 'Kernel_Name', 'Start_Timestamp', 'End_Timestamp')
@@ -57,7 +59,7 @@ def main():
         s[0] += 1
         s[1] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
     total = sum(v[1] for v in st.values())
-    out = {'timed_window_kernels': {
+    out = {'csrc_sha16': a.csrc_sha16, 'commit': a.commit, 'timed_window_kernels': {
         k: {'dispatches': v[0], 'avg_us': v[1] / v[0] / 1e3, 'share': v[1] / total}
         for k, v in sorted(st.items(), key=lambda x: -x[1][1])}}
     for k, v in list(out['timed_window_kernels'].items())[:12]:
