@@ -109,6 +109,35 @@ def test_is_estimator_vs_golden(nat):
         ctx.close()
 
 
+def test_wide_slot_fp64_path_vs_golden(nat, monkeypatch):
+    """The f64-MFMA u-path of wide slots (k_ugemm64, fp64 factor and U; ugemm.hip), forced for
+    every slot (APM_WIDE_Q=0), against the reference's own IS estimates (theta-call and cached
+    u-call), PriorMC estimates and the default fp32 path; a PriorMC slot goes the same way."""
+    for ci, c in enumerate(_cases()):
+        res = {}
+        for env in ({}, {'APM_WIDE_Q': '0'}):
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            ctx = _ctx(nat, c)
+            for k in env:
+                monkeypatch.delenv(k)
+            ctx.u_upload(0, c['ns1'])
+            ctx.u_upload(1, c['ns2'])
+            out, st, _ = ctx.theta_eval(nat.EST_IS, c['theta'][None], [0], [0])
+            out2, st2 = ctx.u_eval([0], [1])
+            pm, st3, _ = ctx.theta_eval(nat.EST_PRIORMC, c['theta'][None], [0], [1])
+            pm2, _ = ctx.u_eval([1], [1])
+            ctx.close()
+            assert st[0] == 0 and st2[0] == 0 and st3[0] == 0
+            res[bool(env)] = (out[0], out2[0], pm[0], pm2[0])
+        ref = (float(c['is_logf1']), float(c['is_logf2']), float(c['pmc_logf1']),
+               float(c['pmc_logf2']))
+        for w, r in zip(res[True], ref):
+            assert _close(w, r), (ci, w, r)
+        for w, f in zip(res[True], res[False]):  # both paths agree far inside the tolerance
+            assert abs(w - f) <= 1e-4, (ci, w, f)
+
+
 def test_cache_tuple_vs_golden(nat):
     """Iterating the API's IS cache yields the reference's (K_chol, C_chol, f_post) tuple
     (estimators.py:166-176); a PriorMC cache converts to the reference's K_chol array
