@@ -1375,9 +1375,10 @@ int apm_slot_read(apm_ctx* c, int64_t slot, double* L, int64_t ldl, double* f_po
             HIPC(hipMemcpyAsync(h.data(), c->Sl.L + slot * c->Sl.lstride, sizeof(float) * h.size(),
                                 hipMemcpyDeviceToHost, c->stream));
             sync(c);
-            if (L)
+            if (L)  // (the slot keeps row i only up to its diagonal tile)
                 for (int i = 0; i < c->n; ++i)
-                    for (int j = 0; j < c->n; ++j) L[(int64_t)i * ldl + j] = h[(size_t)i * np + j];
+                    for (int j = 0; j < c->n; ++j)
+                        L[(int64_t)i * ldl + j] = j <= i ? h[(size_t)i * np + j] : 0.0;
             if (g)
                 for (int j = 0; j < c->n; ++j) g[j] = h[(size_t)np * np + j];
         }

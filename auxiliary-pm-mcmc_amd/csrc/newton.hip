@@ -278,16 +278,19 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
     const int64_t off = (mode == 0) ? np : 0;
     double q = 0.0;  // squared norm of factor row r (the wide-slot test, k_slot_write_vec)
+    // rows stop at the end of their diagonal tile: k_ugemm reads row r up to column
+    // 64 (r / 64 + 1) only (apm_slot_read zeroes the rest on the host)
+    const int cend = (r / 64 + 1) * 64;
     if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
         const double* src = Ab + ((int64_t)np + r) * A.ld;
-        for (int c = lane; c < np; c += 64) {
+        for (int c = lane; c < cend; c += 64) {
             const double x = (c <= r) ? src[np - 1 - c] : 0.0;
             L[c] = (float)x;
             q += x * x;
         }
     } else if (r < np) {
         const double* src = Ab + (off + r) * A.ld + off;
-        for (int c = lane; c < np; c += 64) {
+        for (int c = lane; c < cend; c += 64) {
             const double x = (c <= r) ? src[c] : 0.0;
             L[c] = (float)x;
             q += x * x;
@@ -318,12 +321,13 @@ __global__ __launch_bounds__(256) void k_slot_write_L64(MatB A, SlotSet S,
     const double* Ab = A.base + b * A.cstride;
     double* L = S.L64 + slots[b] * S.l64stride + (int64_t)r * np;
     const int64_t off = (mode == 0) ? np : 0;
+    const int cend = (r / 64 + 1) * 64;  // as k_slot_write_L: k_ugemm64 reads no further
     if (mode == 2) {
         const double* src = Ab + ((int64_t)np + r) * A.ld;
-        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? src[np - 1 - c] : 0.0;
+        for (int c = lane; c < cend; c += 64) L[c] = (c <= r) ? src[np - 1 - c] : 0.0;
     } else {
         const double* src = Ab + (off + r) * A.ld + off;
-        for (int c = lane; c < np; c += 64) L[c] = (c <= r) ? src[c] : 0.0;
+        for (int c = lane; c < cend; c += 64) L[c] = (c <= r) ? src[c] : 0.0;
     }
 }
 

@@ -655,7 +655,9 @@ def main():
                           'hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 accumulation; '
                           'achieved in fp32-equivalent flops against the fp16 peak / 3)',
                           PEAK_F16X3_TFLOPS,
-                          ('k_chol_update32_t128<true>', 'k_chol_update32_t128<false>'), 'f16x3')
+                          ('k_chol_update32_t128<true, false>', 'k_chol_update32_t128<true, true>',
+                           'k_chol_update32_t128<false, false>',  # round-2 names:
+                           'k_chol_update32_t128<true>', 'k_chol_update32_t128<false>'), 'f16x3')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])
