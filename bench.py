@@ -406,23 +406,37 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
     """GPU (every rank) vs oracle (rank 0, broadcast) and vs the reference fixture."""
     import apm_oracle as orc
     B, n = thetas.shape[0], X.shape[0]
-    g1, g2, gops, gst, gf = gpu_parity(X, y, a.n_imp, thetas, U1, U2, rank_device(dist))
+    errors = []
+    # an exception on one rank must not leave the others waiting in a collective: it is
+    # recorded, NaN stands in for the values, and the check fails
+    try:
+        g1, g2, gops, gst, gf = gpu_parity(X, y, a.n_imp, thetas, U1, U2, rank_device(dist))
+    except Exception as e:  # noqa: BLE001
+        errors.append('rank {0} GPU: {1!r}'.format(dist.rank, e))
+        g1 = g2 = gops = np.full(B, np.nan)
+        gst = np.full(B, -1.0)
+        gf = np.full((B, n), np.nan)
     orc_vals = np.zeros((B, 3))
     orc_f = np.zeros((B, n))
     t_orc = 0.
     if dist.rank == 0:
         t0 = time.perf_counter()
-        est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
-        for b in range(B):
-            if b == 0 and oracle_first is not None:  # cpu_baseline's first call pair
-                v1, v2, ops, f = oracle_first
-            else:
-                ops0 = est.n_cubic_ops
-                v1, cache = est(U1, thetas[b])
-                v2, _ = est(U2, None, cache)
-                ops, f = est.n_cubic_ops - ops0, cache[2]
-            orc_vals[b] = (v1, v2, ops)
-            orc_f[b] = f
+        try:
+            est = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8, impl='c'))
+            for b in range(B):
+                if b == 0 and oracle_first is not None:  # cpu_baseline's first call pair
+                    v1, v2, ops, f = oracle_first
+                else:
+                    ops0 = est.n_cubic_ops
+                    v1, cache = est(U1, thetas[b])
+                    v2, _ = est(U2, None, cache)
+                    ops, f = est.n_cubic_ops - ops0, cache[2]
+                orc_vals[b] = (v1, v2, ops)
+                orc_f[b] = f
+        except Exception as e:  # noqa: BLE001
+            errors.append('oracle: {0!r}'.format(e))
+            orc_vals[:] = np.nan
+            orc_f[:] = np.nan
         t_orc = time.perf_counter() - t0
     orc_vals = dist.broadcast(orc_vals)
     orc_f = dist.broadcast(orc_f)
@@ -446,8 +460,12 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
            'oracle': {'theta_call': orc_vals[:, 0].tolist(), 'u_call': orc_vals[:, 1].tolist(),
                       'n_cubic_ops': orc_vals[:, 2].astype(int).tolist(),
                       'seconds': t_orc if dist.rank == 0 else None}}
-    ok = (out['d_theta_call'] <= PARITY_TOL_NATS and out['d_u_call'] <= PARITY_TOL_NATS and
-          out['n_cubic_ops_equal'] and out['status_ok'] and out['f_post_max_rel'] <= PARITY_FPOST_REL)
+    n_err = dist.sum(len(errors))
+    if errors:
+        out['errors'] = errors
+    ok = (n_err == 0 and out['d_theta_call'] <= PARITY_TOL_NATS and
+          out['d_u_call'] <= PARITY_TOL_NATS and out['n_cubic_ops_equal'] and out['status_ok'] and
+          out['f_post_max_rel'] <= PARITY_FPOST_REL)
     z, why = reference_fixture(X, y, a.n, a.d, a.n_imp, a.seed)
     ref = {'fixture': os.path.relpath(REF_FIXTURE, REPO), 'used': z is not None, 'why': why}
     if z is not None:
@@ -715,8 +733,12 @@ def main():
     cpu, first = None, None
     thetas_par, U1, U2 = parity_inputs(a.n, a.d, a.n_imp)
     if a.cpu_baseline and dist.rank == 0:
-        cpu, first = cpu_baseline(X, y, a.n_imp, thetas_par[0], n_th, n_u, a.cpu_budget, U1, U2)
-        cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
+        try:  # (rank 0 alone: a failure here must not strand the others in the parity check)
+            cpu, first = cpu_baseline(X, y, a.n_imp, thetas_par[0], n_th, n_u, a.cpu_budget,
+                                      U1, U2)
+            cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
+        except Exception as e:  # noqa: BLE001
+            cpu, first = {'error': repr(e)}, None
     parity = parity_check(dist, X, y, a, thetas_par, U1, U2, first) if a.parity else None
 
     # per-rank record: device, chains, transitions, elapsed (8 distinct devices, even load)
