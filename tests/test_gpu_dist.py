@@ -34,6 +34,11 @@ def test_bench_two_ranks_on_one_gpu(gpu_available):
     assert line['transitions_timed'] >= 2 * 4 * 4
     assert line['value'] > 0 and line['ms_per_step'] > 0
     assert line['ess_sample']['chains'] == 8
+    # both ranks' GPU values checked against rank 0's oracle (gathered over gloo)
+    assert line['parity']['pass'] and line['parity']['checked_ranks'] == 2
+    assert line['parity']['vs_reference']['used'] is False  # N=1024: not the fixture's workload
+    assert [r['rank'] for r in line['ranks']] == [0, 1]
+    assert sum(r['transitions'] for r in line['ranks']) == line['transitions_timed']
 
 
 def test_config3_rank_shares_consistent(gpu_available):
