@@ -53,10 +53,12 @@ void launch_chol_update(MatB A, int k0, int kc, const unsigned* tiles, int ntile
                         FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
 // the same with one 128x128 super-tile per workgroup (tiles from build_update_supertiles)
 // plus: 0 A -= ..., 1 A += ..., 2 A = I + Y Y^T for lower-triangular Y (depth per tile column
-// truncated to the nonzero blocks; the old tile is not read)
+// truncated to the nonzero blocks; the old tile is not read). S.base: the old tiles are read from
+// S (same tile coordinates, own ld / chain stride) instead of A - an out-of-place update
 void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int plus,
                              Live live, int nchains, hipStream_t s,
-                             FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0});
+                             FusedDiag<double> fd = FusedDiag<double>{0, nullptr, 0, nullptr, 0, 0},
+                             MatB S = MatB{nullptr, 0, 0});
 long update_tile_count(int i0, int R, int j0, int jend);
 #include <vector>
 std::vector<unsigned> build_update_tiles(int i0, int R, int j0, int jend, int glo = 0, int ghi = 0);
@@ -136,10 +138,11 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 // ---- gram.hip -------------------------------------------------------------------------------
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
 // kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
-// both: write both triangles (else K's lower tiles only); K2.base: the lower tiles also to K2
+// both: write both triangles (else K's lower tiles only); K2.base: the lower tiles of tile
+// columns < k2cols also to K2
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0});
+                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30);
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)

@@ -120,7 +120,10 @@ struct apm_ctx {
     int *active2 = nullptr, *status2 = nullptr;
     // chol(K) is enqueued one outer panel at a time, each released when the main stream enters a
     // single-workgroup-per-chain TRSV (3/4 of the CUs idle) - see feed_chol_k
-    int cholk_next = -1, cholk_count = 0;  // single-launch TRSV per solve (APM_TRSV_FUSED=0: a launch per block)  // left-looking updates inside an outer panel (APM_LEFT=0: right)
+    int cholk_next = -1, cholk_count = 0;
+    // the Gram wrote only the first outer panel's tile columns into chol(K)'s working copy: the
+    // first trailing update then reads its old tiles from K (out of place, k_chol_update_t128 S)
+    bool cholk_partial = false;
 };
 
 namespace {
@@ -260,10 +263,14 @@ std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend
 
 void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, int jend, Gap g,
                     int plus, int count, int fuse_k = -1, int fail_code = 0,
-                    const Exec* ex = nullptr) {
+                    const Exec* ex = nullptr, const MatB* src = nullptr) {
     const Exec E = ex ? *ex : main_exec(c);
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
+    const bool t128 =
+        (c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k));
+    if (src && (!t128 || c->ozaki || plus == 2))  // (theta_eval_impl enables it only where it holds)
+        throw HipError{"out-of-place update needs the fp64 t128 path"};
     const auto tl = tile_list(c, i0, R, j0, jend, g);
     if (tl.second <= 0) return;
     FusedDiag<double> fd{0, nullptr, 0, nullptr, 0, 0};
@@ -271,7 +278,7 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, g, plus == 2) * E.live_n : 0.0;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE, fl, E.s);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
-    if ((c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
+    if (t128) {
         const auto sl = super_list(c, i0, R, j0, jend, g);
         if (c->ozaki && plus != 2 && kc <= OUTER && kc % 4 == 0 &&
             (int64_t)(R - j0) * 64 <= c->oz_rows) {
@@ -285,7 +292,8 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
             check_launch();
             launch_oz_update_t128(M, P, depth, sl.first, sl.second, plus, E.lv, count, E.s, fd);
         } else {
-            launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd);
+            launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd,
+                                    src ? *src : MatB{nullptr, 0, 0});
         }
     } else {
         if (plus == 2) throw HipError{"identity-initialised update needs the t128 path"};
@@ -304,7 +312,7 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
 void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
                 bool factor_diag = true, int row_start = 0, GapFn gap = no_gap,
-                const Exec* ex = nullptr) {
+                const Exec* ex = nullptr, const MatB* first_src = nullptr) {
     const Exec E = ex ? *ex : main_exec(c);
     const Live lv = E.lv;
     const bool fuse = factor_diag && c->fuse_diag && row_start <= k0;
@@ -330,7 +338,7 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
             }
             have_diag = Kend < k1;
             tracked_update(c, M, K, Kend - K, Kend, R, Kend, Cb, gap(Kend - 1, c->nb), false,
-                           count, have_diag ? Kend : -1, fail_code, &E);
+                           count, have_diag ? Kend : -1, fail_code, &E, K == k0 ? first_src : nullptr);
             continue;
         }
         for (int k = K; k < Kend; ++k) {
@@ -349,7 +357,8 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
         }
         have_diag = fuse && Kend < k1;
         tracked_update(c, M, K, Kend - K, std::max(Kend, row_start), R, Kend, Cb,
-                       gap(Kend - 1, c->nb), false, count, have_diag ? Kend : -1, fail_code, &E);
+                       gap(Kend - 1, c->nb), false, count, have_diag ? Kend : -1, fail_code, &E,
+                       K == k0 ? first_src : nullptr);
     }
 }
 
@@ -745,17 +754,21 @@ Exec k_exec(apm_ctx* c, hipStream_t s);
 void chol_k_panel(apm_ctx* c, const Exec& ex) {
     const int K = c->cholk_next;
     if (K < 0 || K >= c->nb) return;
+    // first panel after a partial Gram copy: the trailing update reads K's tiles (out of place)
+    const MatB* src = (K == 0 && c->cholk_partial) ? &c->K : nullptr;
     chol_range(c, bl_of(c), K, std::min(K + OUTER, c->nb), c->nb, c->nb, APM_STATUS_CHOL_K,
-               c->cholk_count, true, 0, no_gap, &ex);
+               c->cholk_count, true, 0, no_gap, &ex, src);
     c->cholk_next = K + OUTER;
 }
-void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true) {
+void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true, bool partial = false) {
     HIPC(hipMemsetD32Async(c->active2, 1, count, ex.s));
     HIPC(hipMemsetAsync(c->status2, 0, sizeof(int) * count, ex.s));
-    if (copy) {  // (else the Gram wrote K's lower tiles into BL as well)
+    if (copy) {  // (else the Gram wrote K's lower tiles into BL as well, or those of the first
+                 // outer panel's tile columns: partial)
         launch_copy_lower(c->K, bl_of(c), c->np, ex.lv, count, ex.s);
         check_launch();
     }
+    c->cholk_partial = !copy && partial;
     c->cholk_next = 0;
     c->cholk_count = count;
     chol_k_panel(c, ex);
@@ -844,9 +857,17 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     // the matrix a factorisation of K starts from (chol(K)'s working copy BL, or PriorMC's A):
     // the Gram writes K's lower tiles there too instead of a later copy pass (APM_GRAM2=0: copy)
     MatB k2{nullptr, 0, 0};
+    int k2cols = 1 << 30;
     if (gram && c->gram2 && !c->postcov_aug) {
-        if (est == APM_EST_PRIORMC) k2 = c->A;
-        else if (ov) k2 = bl_of(c);
+        if (est == APM_EST_PRIORMC) {
+            k2 = c->A;
+        } else if (ov) {
+            k2 = bl_of(c);
+            // chol(K)'s first trailing update can read its old tiles from K (out of place): the
+            // Gram then copies only the first outer panel's tile columns (~1/4 of the lower tiles
+            // at N = 4096 instead of all of them)
+            if ((c->t128 & 2) && !c->ozaki && OUTER >= 2 && c->nb - OUTER >= 2) k2cols = OUTER;
+        }
     }
     if (gram) {
         // the augmented posterior route (APM_POSTCOV=aug) reads K's upper tiles; every other
@@ -855,7 +876,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         const double nk = c->k_full ? (double)c->n * c->n : 0.5 * (double)c->n * (c->n + 1);
         ProfScope ps(c, APM_PROF_GRAM, 8.0 * ((double)c->n * c->d + nk) * count + 8.0 * c->P);
         launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
-                    count, c->stream, c->k_full, k2);
+                    count, c->stream, c->k_full, k2, k2cols);
         check_launch();
     }
     std::vector<int> st_h(count, 0), it_h(count, 0);
@@ -873,7 +894,8 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         if (ov) {
             HIPC(hipEventRecord(c->ev_gram, c->stream));
             HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
-            chol_k_begin(c, count, k_exec(c, c->stream2), /*copy=*/k2.base == nullptr);
+            chol_k_begin(c, count, k_exec(c, c->stream2), /*copy=*/k2.base == nullptr,
+                         /*partial=*/k2cols < c->nb);
         }
         const int64_t reruns = c->n_fp64_rerun;
         if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself

@@ -382,7 +382,7 @@ struct __attribute__((aligned(16))) GemmSmem64T {
 template <bool NEG, bool INIT = false>
 __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigned e, int b,
                                                  bool fused, Live live, FusedDiag<double> fd,
-                                                 GemmSmem64T& smg, DiagSmem& smd) {
+                                                 GemmSmem64T& smg, DiagSmem& smd, MatB S) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     const int ti = (int)(e >> 18), tj = (int)((e >> 4) & 0x3fff);
@@ -449,7 +449,10 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
     // old tile into acc (negated for A_ij -= ...: acc = -C + sum, result = -acc), consumed before
     // the loop so that no wait for it lands inside (see k_chol_update32_t128)
     const int li = mine ? oi : (wr ? ra1 : ra0), lj = mine ? oj : (wc ? cb1 : cb0);
-    const double* Cw = Ab + (int64_t)(li * 64) * A.ld + lj * 64;
+    // (S.base: out of place - the old tile comes from S, e.g. K for the first trailing update of
+    // chol(K), whose working copy holds the first outer panel only: capi.cpp chol_k_begin)
+    const int64_t cld = S.base ? S.ld : A.ld;
+    const double* Cw = (S.base ? S.base + b * S.cstride : Ab) + (int64_t)(li * 64) * cld + lj * 64;
 #pragma unroll
     for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
@@ -462,7 +465,7 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
                                                                                           : 0.0;
                     continue;
                 }
-                const double v = Cw[(int64_t)(16 * bi + F64_CROW(lane, r)) * A.ld + 16 * bj + r16];
+                const double v = Cw[(int64_t)(16 * bi + F64_CROW(lane, r)) * cld + 16 * bj + r16];
                 acc[bi][bj][r] = NEG ? -v : v;
             }
 #pragma unroll
@@ -527,7 +530,8 @@ __device__ __forceinline__ void update_t128_body(MatB A, int k0, int kc, unsigne
 __global__ __launch_bounds__(256, 2) void k_chol_update_t128(MatB A, int k0, int kc,
                                                              const unsigned* __restrict__ tiles,
                                                              int ntiles, int nchains, int plus,
-                                                             Live live, FusedDiag<double> fd) {
+                                                             Live live, FusedDiag<double> fd,
+                                                             MatB S) {
     __shared__ union {
         GemmSmem64T g;
         DiagSmem d;
@@ -546,19 +550,20 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_t128(MatB A, int k0, int
     }
     if (!chain_live(live, b)) return;
     if (plus == 2)  // A_ij = I_ij + Y_i Y_j^T (the SYRK of the UL factorisation, postcov.hip)
-        update_t128_body<false, true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+        update_t128_body<false, true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d, S);
     else if (plus)  // A_ij += ...
-        update_t128_body<false>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+        update_t128_body<false>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d, S);
     else
-        update_t128_body<true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d);
+        update_t128_body<true>(A, k0, kc, tiles[t], b, fused, live, fd, sm.g, sm.d, S);
 }
 
 void launch_chol_update_t128(MatB A, int k0, int kc, const unsigned* tiles, int ntiles, int plus,
-                             Live live, int nchains, hipStream_t s, FusedDiag<double> fd) {
+                             Live live, int nchains, hipStream_t s, FusedDiag<double> fd,
+                             MatB S) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     hipLaunchKernelGGL(k_chol_update_t128, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc,
-                       tiles, ntiles, nchains, plus, live, fd);
+                       tiles, ntiles, nchains, plus, live, fd, S);
 }
 
 // Host: tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in super-tile order (SxS tiles,
