@@ -47,6 +47,13 @@ def main(path):
     ends = preps[1:] + [rows[last_newton][1]]
     print('newton iterations (ms): ' + ' '.join('{0:.1f}'.format((e - a) / 1e6)
                                                 for a, e in zip(preps, ends)))
+    post = collections.defaultdict(lambda: [0.0, 0])
+    for s, e, n, q in rows[first_post:slot]:
+        post[n][0] += (e - s) / 1e6
+        post[n][1] += 1
+    print('posterior factor kernels (main stream, ms / launches):')
+    for n, (v, c) in sorted(post.items(), key=lambda x: -x[1][0])[:8]:
+        print('  {0:40s} {1:8.2f} ms {2:5d}'.format(n[:40], v, c))
     top = collections.defaultdict(float)
     for s, e, n, q in rows[:end + 1]:
         top[(n, 'main' if q == main_q else 's2')] += (e - s) / 1e6
