@@ -331,6 +331,9 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 // it in fp64).
 #define DF_FAILED 15
 #define DF_SPIN (1 << 22)
+#ifndef DF_UNROLLED
+#define DF_UNROLLED true
+#endif
 // DF_TRACE (diagnostic builds only, tools/df_trace.py): wall-clock stamps of chain 0's first
 // outer panel, [row - K][column - K][event], read back by apm_debug_df_trace
 #ifdef DF_TRACE
@@ -363,7 +366,10 @@ __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float*
                                    acc[bi][bj][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
+#ifndef DF_WPE
+#define DF_WPE 2  // min workgroups per CU of the dataflow panel kernel
+#endif
+__global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
                                                          FusedDiag<float> fd, Live live, int hlim,
                                                          const int* __restrict__ h3ok,
                                                          unsigned long long* prog,
@@ -497,7 +503,7 @@ __global__ __launch_bounds__(256) void k_chol_panel_df32(MatF A, int K, int ncol
             __syncthreads();
             DF_STAMP(5);
             if (wv == 0) {
-                const bool ok = diag_compute<true, float>(sm.d, lane);
+                const bool ok = diag_compute<DF_UNROLLED, float>(sm.d, lane);
                 if (lane == 0) sm.d.ok = ok;
             }
             __syncthreads();
