@@ -139,10 +139,12 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
 // kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
 // both: write both triangles (else K's lower tiles only); K2.base: the lower tiles of tile
-// columns < k2cols also to K2
+// columns < k2cols also to K2; mfma: the GEMM-form distances on the f64 MFMA (k_gram_mfma),
+// else the direct form on the VALU (k_gram)
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30);
+                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30,
+                 bool mfma = true);
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)
@@ -252,6 +254,8 @@ struct UPool {
                         // fp32 values; host uploads keep their fp64 values for the wide path)
     int64_t stride;
     int sp;
+    float* base32;      // the same buffers rounded to fp32 (same layout), written with them: the
+                        // operand k_ugemm reads (half the bytes of converting the fp64 ones there)
 };
 void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int64_t ubuf,
                       hipStream_t s);

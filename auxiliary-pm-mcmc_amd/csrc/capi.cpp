@@ -90,6 +90,7 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
     bool gram2 = true;    // APM_GRAM2=0: K's working copies by k_copy_lower instead of the Gram
+    bool gram_mfma = true;  // APM_GRAM_MFMA=0: the direct-form Gram on the VALU (k_gram)
     // fp64 outer (rank-64*OUTER) trailing updates on int8 MFMA (ozaki.hip, APM_OZAKI); one
     // residue-plane buffer per stream (the concurrent chol(K) runs on stream2)
     bool ozaki = false;
@@ -876,7 +877,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         const double nk = c->k_full ? (double)c->n * c->n : 0.5 * (double)c->n * (c->n + 1);
         ProfScope ps(c, APM_PROF_GRAM, 8.0 * ((double)c->n * c->d + nk) * count + 8.0 * c->P);
         launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
-                    count, c->stream, c->k_full, k2, k2cols);
+                    count, c->stream, c->k_full, k2, k2cols, c->gram_mfma);
         check_launch();
     }
     std::vector<int> st_h(count, 0), it_h(count, 0);
@@ -987,6 +988,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_EXPORT")) c->export_rb = atoi(e) != 0;
     if (const char* e = getenv("APM_RHS_ROW")) c->rhs_row = atoi(e) != 0;
     if (const char* e = getenv("APM_GRAM2")) c->gram2 = atoi(e) != 0;
+    if (const char* e = getenv("APM_GRAM_MFMA")) c->gram_mfma = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
     if (const char* e = getenv("APM_OZAKI")) c->ozaki = atoi(e) != 0;
@@ -1105,8 +1107,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     HIPC(hipMemset(c->Sl.cst, 0, sizeof(double) * n_slots));
     HIPC(hipMemset(c->Sl.wide, 0, sizeof(int) * n_slots));
     c->slot_wide.assign((size_t)n_slots, 0);
-    c->Up = UPool{dalloc<double>(c, n_ubufs * np * c->sp), np * c->sp, c->sp};
+    c->Up = UPool{dalloc<double>(c, n_ubufs * np * c->sp), np * c->sp, c->sp,
+                  dalloc<float>(c, n_ubufs * np * c->sp)};
     HIPC(hipMemset(c->Up.base, 0, sizeof(double) * n_ubufs * np * c->sp));
+    HIPC(hipMemset(c->Up.base32, 0, sizeof(float) * n_ubufs * np * c->sp));
 }
 
 void free_ctx(apm_ctx* c) {
@@ -1443,8 +1447,10 @@ int apm_gram(int device, int kind, const double* X, int64_t n, int64_t d, int64_
         HIPC(hipMemcpyAsync(c->theta, theta, sizeof(double) * P, hipMemcpyHostToDevice, c->stream));
         HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+        // (the cached context's knob, re-read per call: tests compare both kernels)
+        if (const char* e = getenv("APM_GRAM_MFMA")) c->gram_mfma = atoi(e) != 0;
         launch_gram(c->K, c->X, d, (int)n, (int)d, c->theta, P, kind, eps, c->np, live_of(c), 1,
-                    c->stream, true);
+                    c->stream, true, MatB{nullptr, 0, 0}, 1 << 30, c->gram_mfma);
         check_launch();
         HIPC(hipMemcpy2DAsync(K, sizeof(double) * ldk, c->K.base, sizeof(double) * c->np,
                               sizeof(double) * n, n, hipMemcpyDeviceToHost, c->stream));

@@ -14,12 +14,14 @@
 
 // ------------------------------------------------------------------------------- U buffers
 __global__ __launch_bounds__(256) void k_u_convert(const double* __restrict__ U, int64_t ldu,
-                                                   int n, int S, double* __restrict__ dst, int sp,
-                                                   int np) {
+                                                   int n, int S, double* __restrict__ dst,
+                                                   float* __restrict__ dst32, int sp, int np) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= (int64_t)np * sp) return;
     const int r = (int)(e / sp), c = (int)(e % sp);
-    dst[e] = (r < n && c < S) ? U[(int64_t)r * ldu + c] : 0.0;
+    const double v = (r < n && c < S) ? U[(int64_t)r * ldu + c] : 0.0;
+    dst[e] = v;
+    dst32[e] = (float)v;
 }
 
 void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int64_t ubuf,
@@ -27,7 +29,7 @@ void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int
     const int np = (int)(P.stride / P.sp);
     const int64_t tot = (int64_t)np * P.sp;
     hipLaunchKernelGGL(k_u_convert, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, U64, ldu,
-                       n, S, P.base + ubuf * P.stride, P.sp, np);
+                       n, S, P.base + ubuf * P.stride, P.base32 + ubuf * P.stride, P.sp, np);
 }
 
 // Philox4x32-10 (Salmon et al., SC'11) + Box-Muller: counter = (e/4, ctr_lo, ctr_hi, 0)
@@ -85,10 +87,14 @@ __global__ __launch_bounds__(256) void k_u_normal(UPool P, const int64_t* __rest
         z[2 * h + 1] = rr * sn;
     }
     double* dst = P.base + ubufs[b] * P.stride;
+    float* dst32 = P.base32 + ubufs[b] * P.stride;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
         const int64_t e = q * 4 + h;
-        if (e < tot) dst[(e / S) * P.sp + (e % S)] = (double)z[h];
+        if (e < tot) {
+            dst[(e / S) * P.sp + (e % S)] = (double)z[h];
+            dst32[(e / S) * P.sp + (e % S)] = z[h];
+        }
     }
 }
 
@@ -108,7 +114,9 @@ __global__ __launch_bounds__(256) void k_u_combine(UPool P, const int64_t* __res
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= tot) return;
     const double x = P.base[a[b] * P.stride + e], v = P.base[bb[b] * P.stride + e];
-    P.base[dst[b] * P.stride + e] = ca[b] * x + cb[b] * v;
+    const double u = ca[b] * x + cb[b] * v;
+    P.base[dst[b] * P.stride + e] = u;
+    P.base32[dst[b] * P.stride + e] = (float)u;
 }
 
 void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64_t* b,
@@ -131,6 +139,10 @@ __device__ __forceinline__ double is_term(double f, double y, double W, double z
     return log_ndtr_mixed(y * f) + (0.5 * W * f - z) * f;
 }
 
+// NSW sample blocks per workgroup (64 x 64 NSW output tile, waves 32 x 32 NSW): NSW = 2 reads L
+// once per two sample blocks (batches of >= UGEMM_W2_MIN chains), NSW = 1 keeps 4x the
+// workgroups for the small batches whose heaviest row block bounds the launch.
+template <int NSW>
 __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restrict__ slots,
                                                UPool P, const int64_t* __restrict__ ubufs,
                                                const double* __restrict__ y, int n, int np,
@@ -144,46 +156,48 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     // workgroups that share row block i's slice of L run together on one XCD and read it once
     // from its L2, and a chain's U stays within one XCD's L2 / the Infinity Cache.
     const int nb = np / 64;
-    const long total = (long)nb * nsb * nchains;
+    const int nsg = nsb / NSW;  // sample groups
+    const long total = (long)nb * nsg * nchains;
     const long slot_id = blockIdx.x, xcd = slot_id & 7, q = total >> 3, rem = total & 7;
     const long item = nchains < 8 ? slot_id  // too few chains to fill 8 XCDs evenly: plain order
                       : (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (slot_id >> 3);
-    const int b = (int)(item / ((long)nb * nsb));
-    const int rest = (int)(item % ((long)nb * nsb));
+    const int b = (int)(item / ((long)nb * nsg));
+    const int rest = (int)(item % ((long)nb * nsg));
     if (status[b] != 0) return;
-    const int i = nb - 1 - rest / nsb;
-    const int sb = rest % nsb;
+    const int i = nb - 1 - rest / nsg;
+    const int sb = (rest % nsg) * NSW;  // first sample block
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
     const int r16 = lane & 15, kq = lane >> 4;
-    __shared__ float Ut[2][64][UP];
-    __shared__ double csum[2][64];
+    constexpr int SW = 64 * NSW;  // samples per workgroup
+    __shared__ float Ut[2][64][SW + 1];
+    __shared__ double csum[2][SW];
 
     const int64_t slot = slots[b];
     if (S.wide[slot]) return;  // k_ugemm64
     const float* L = S.L + slot * S.lstride;
-    const double* U = P.base + ubufs[b] * P.stride;
+    const float* U = P.base32 + ubufs[b] * P.stride;
     const int sp = P.sp;
     const int kend = (i + 1) * 64;
 
-    f4_t acc[2][2];
+    f4_t acc[2][2 * NSW];
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+        for (int bj = 0; bj < 2 * NSW; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
 
-    // U[kk:kk+64][sb*64 : sb*64+64] (16 KB, 16-byte loads) and the A fragments (straight from
-    // global: 16 contiguous floats per lane and row) of the next slice are loaded into registers
-    // while the current one is multiplied; U goes through two LDS buffers, one barrier per slice
-    f4_t un[4];
+    // U[kk:kk+64][sb*64 : sb*64+SW] (16 KB per sample block, 16-byte loads) and the A fragments
+    // (straight from global: 16 contiguous floats per lane and row) of the next slice are loaded
+    // into registers while the current one is multiplied; U goes through two LDS buffers, one
+    // barrier per slice
+    constexpr int PR = 16 * NSW;  // 16-byte pieces per U row
+    f4_t un[4 * NSW];
     f4_t an[2][4];
     auto gload = [&](int kk) {
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const int e = tid + h * 256;  // 4-element piece 0..1023
-            const double* pu = U + (int64_t)(kk + (e >> 4)) * sp + sb * 64 + (e & 15) * 4;
-            const d2_t u0 = *reinterpret_cast<const d2_t*>(pu);
-            const d2_t u1 = *reinterpret_cast<const d2_t*>(pu + 2);
-            un[h] = f4_t{(float)u0[0], (float)u0[1], (float)u1[0], (float)u1[1]};
+        for (int h = 0; h < 4 * NSW; ++h) {
+            const int e = tid + h * 256;  // 4-element piece
+            un[h] = *reinterpret_cast<const f4_t*>(U + (int64_t)(kk + e / PR) * sp + sb * 64 +
+                                                   (e % PR) * 4);
         }
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
@@ -195,9 +209,9 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     gload(0);
     for (int kk = 0, cur = 0; kk < kend; kk += 64, cur ^= 1) {
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
+        for (int h = 0; h < 4 * NSW; ++h) {
             const int e = tid + h * 256;
-            const int r = e >> 4, c4 = (e & 15) * 4;
+            const int r = e / PR, c4 = (e % PR) * 4;
             Ut[cur][r][c4] = un[h][0];
             Ut[cur][r][c4 + 1] = un[h][1];
             Ut[cur][r][c4 + 2] = un[h][2];
@@ -212,13 +226,14 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
         if (kk + 64 < kend) gload(kk + 64);
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            float bv[2];
+            float bv[2 * NSW];
 #pragma unroll
-            for (int bj = 0; bj < 2; ++bj) bv[bj] = Ut[cur][kq * 16 + t][32 * wc + 16 * bj + r16];
+            for (int bj = 0; bj < 2 * NSW; ++bj)
+                bv[bj] = Ut[cur][kq * 16 + t][32 * NSW * wc + 16 * bj + r16];
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-                for (int bj = 0; bj < 2; ++bj)
+                for (int bj = 0; bj < 2 * NSW; ++bj)
                     acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi][t], bv[bj],
                                                                        acc[bi][bj], 0, 0, 0);
         }
@@ -228,9 +243,9 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     const double* fp = S.fpost64 + slot * S.vstride;
     const double* Wv = S.W64 + slot * S.vstride;
     const double* zv = S.z64 + slot * S.vstride;
-    double colsum[2];
+    double colsum[2 * NSW];
 #pragma unroll
-    for (int bj = 0; bj < 2; ++bj) {
+    for (int bj = 0; bj < 2 * NSW; ++bj) {
         double d = 0.0;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
@@ -244,11 +259,11 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
         colsum[bj] = d;
     }
     if (kq == 0) {
-        csum[wr][32 * wc + r16] = colsum[0];
-        csum[wr][32 * wc + 16 + r16] = colsum[1];
+#pragma unroll
+        for (int bj = 0; bj < 2 * NSW; ++bj) csum[wr][32 * NSW * wc + 16 * bj + r16] = colsum[bj];
     }
     __syncthreads();
-    if (tid < 64) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
+    if (tid < SW) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
 }
 
 // The same product and epilogue on f64 MFMA (v_mfma_f64_16x16x4_f64) for the call's WIDE slots
@@ -329,13 +344,25 @@ __global__ __launch_bounds__(256) void k_ugemm64(SlotSet S, const int64_t* __res
     if (tid < 64) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
 }
 
+static int UGEMM_W2_MIN = -1;  // batches >= this many chains take k_ugemm<2> (APM_UGEMM_W2_MIN)
+
 void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
                   const double* y, int n, int np, double* partial, int64_t pstride,
                   const int* status, int nchains, bool wide, hipStream_t s) {
+    if (UGEMM_W2_MIN < 0) {
+        const char* e = getenv("APM_UGEMM_W2_MIN");
+        UGEMM_W2_MIN = e ? atoi(e) : 1 << 30;
+    }
     const int nb = np / 64, nsb = P.sp / 64;
-    const long total = (long)nb * nsb * nchains;
-    hipLaunchKernelGGL(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
-                       np, partial, pstride, status, nsb, nchains);
+    if (nchains >= UGEMM_W2_MIN && nsb % 2 == 0) {
+        const long total = (long)nb * (nsb / 2) * nchains;
+        hipLaunchKernelGGL(k_ugemm<2>, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs,
+                           y, n, np, partial, pstride, status, nsb, nchains);
+    } else {
+        const long total = (long)nb * nsb * nchains;
+        hipLaunchKernelGGL(k_ugemm<1>, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs,
+                           y, n, np, partial, pstride, status, nsb, nchains);
+    }
     if (wide)
         hipLaunchKernelGGL(k_ugemm64, dim3((unsigned)(nb * nsb), nchains), dim3(256), 0, s, S,
                            slots, P, ubufs, y, n, np, partial, pstride, status, nsb);

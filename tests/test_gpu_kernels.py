@@ -76,6 +76,26 @@ def test_gram_large_ragged_vs_c_oracle(nat):
         _assert_gram_close(K, Kr)
 
 
+def test_gram_mfma_fixups_vs_c_oracle(nat, monkeypatch):
+    """k_gram_mfma's direct-form fix-ups (pairs whose GEMM-form distance cancels): near-duplicate
+    rows, D within one LDS chunk (fix-ups from LDS) and beyond it (from global X), iso and ARD;
+    the direct-form kernel (APM_GRAM_MFMA=0) against the same oracle."""
+    rng = np.random.RandomState(11)
+    for n, d, kind in ((200, 3, 'ard'), (150, 40, 'ard'), (130, 6, 'iso')):
+        base = rng.normal(size=(n // 2, d))
+        X = np.concatenate([base, base + 1e-4 * rng.normal(size=base.shape)])[rng.permutation(n)]
+        X = np.concatenate([X, 3.0 + 0.01 * rng.normal(size=(n % 2, d))]) if n % 2 else X
+        th = np.r_[0.2, rng.normal(scale=0.5, size=d if kind == 'ard' else 1)]
+        Kr = np.empty((n, n))
+        orc.c_gram(kind, Kr, X, th, 1e-8)
+        for mfma in ('1', '0'):
+            monkeypatch.setenv('APM_GRAM_MFMA', mfma)
+            K = np.empty((n, n))
+            nat.gram(nat.KERNEL_ISO if kind == 'iso' else nat.KERNEL_ARD, K, X, th, 1e-8)
+            _assert_gram_close(K, Kr)
+            assert np.array_equal(K, K.T)
+
+
 def test_laplace_vs_golden(nat):
     for c in _cases():
         f, C, lml, nit, st = nat.laplace(c['K'], c['y'], True, True, 1e-4, 1000)

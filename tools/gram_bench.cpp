@@ -34,23 +34,39 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     const int k2c[2] = {8, 0};
+    std::vector<double> Kh[2];
+    for (int mf = 0; mf < 2; ++mf)
     for (int v = 0; v < 2; ++v) {
         for (int w = 0; w < 3; ++w)
             launch_gram(MK, X, d, n, d, th, P, 1, 1e-8, np, lv, chains, 0, false,
-                        k2c[v] ? MK2 : MatB{nullptr, 0, 0}, k2c[v]);
+                        k2c[v] ? MK2 : MatB{nullptr, 0, 0}, k2c[v], mf);
         hipEventRecord(e0, 0);
         const int reps = 10;
         for (int r = 0; r < reps; ++r)
             launch_gram(MK, X, d, n, d, th, P, 1, 1e-8, np, lv, chains, 0, false,
-                        k2c[v] ? MK2 : MatB{nullptr, 0, 0}, k2c[v]);
+                        k2c[v] ? MK2 : MatB{nullptr, 0, 0}, k2c[v], mf);
         hipEventRecord(e1, 0);
         hipEventSynchronize(e1);
         float ms;
         hipEventElapsedTime(&ms, e0, e1);
         ms /= reps;
         const double bytes = 8.0 * ((double)n * (n + 1) / 2) * chains;
-        printf("ABL=%d k2cols=%d chains=%d d=%d: %.3f ms  %.2f TB/s (lower-tile bytes)\n", GRAM_ABL,
-               k2c[v], chains, d, ms, bytes / (ms * 1e-3) / 1e12);
+        printf("%s ABL=%d k2cols=%d chains=%d d=%d: %.3f ms  %.2f TB/s (lower-tile bytes)\n",
+               mf ? "k_gram_mfma" : "k_gram     ", GRAM_ABL, k2c[v], chains, d, ms,
+               bytes / (ms * 1e-3) / 1e12);
+        if (v == 0) {  // last chain's K: GEMM form vs direct form (lower triangle)
+            Kh[mf].resize((size_t)cs);
+            hipMemcpy(Kh[mf].data(), K + (chains - 1) * cs, sizeof(double) * cs,
+                      hipMemcpyDeviceToHost);
+        }
     }
+    double worst = 0.0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            const double a = Kh[1][(size_t)i * np + j], r = Kh[0][(size_t)i * np + j];
+            const double sc = fmax(1.0, fabs(log(fmax(r, 1e-300))));
+            worst = fmax(worst, fabs(a - r) / (sc * fabs(r) + 1e-300));
+        }
+    printf("GEMM form vs direct form: max |dK| / (K max(1, |log K|)) = %.3g\n", worst);
     return 0;
 }
