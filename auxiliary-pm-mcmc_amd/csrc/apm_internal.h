@@ -144,7 +144,7 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
                  hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30,
-                 bool mfma = true);
+                 bool mfma = false);
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)

@@ -90,7 +90,10 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
     bool gram2 = true;    // APM_GRAM2=0: K's working copies by k_copy_lower instead of the Gram
-    bool gram_mfma = true;  // APM_GRAM_MFMA=0: the direct-form Gram on the VALU (k_gram)
+    // APM_GRAM_MFMA=1: the GEMM-form Gram on the f64 MFMA (k_gram_mfma: -8 % kernel time, but
+    // the K of the ill-conditioned sigma = e^18.5 fixture moves its estimate outside twice the
+    // reference's own spread); default: the reference's direct form (k_gram)
+    bool gram_mfma = false;
     // fp64 outer (rank-64*OUTER) trailing updates on int8 MFMA (ozaki.hip, APM_OZAKI); one
     // residue-plane buffer per stream (the concurrent chol(K) runs on stream2)
     bool ozaki = false;

@@ -223,44 +223,105 @@ __global__ __launch_bounds__(256, 2) void k_gram_mfma(MatB K, const double* __re
         }
     }
     __syncthreads();  // norms complete
-    if (!mine) return;
 
     // f64 MFMA output map: lane l, reg r -> row (l >> 4) + 4r, col l & 15 of block (p, q)
+    if (mine) {
+        // (1) GEMM-form distances; a bit per pair whose subtraction cancels
+        unsigned long long fix = 0;
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < 4; ++p)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int li = ro + 16 * p + kq + 4 * r, lj = co + 16 * q + r16;
-                const int gi = si * 128 + li, gj = sj * 128 + lj;
-                const double ni = nrm[0][li], nj = nrm[1][lj];
-                double s = ni + nj - 2.0 * acc[p][q][r];
-                if (s < 0.5 * (ni + nj) && gi != gj && gi < n && gj < n) {
-                    // direct form, the k_gram arithmetic (rare; divergent)
-                    s = 0.0;
-                    if (d <= GK) {
-                        for (int k = 0; k < d; ++k) {
-                            const double df = zi[k][li] - zj[k][lj];
-                            s = fma(df, df, s);
-                        }
-                    } else {
-                        const double* xa = X + (int64_t)gi * ldx;
-                        const double* xc = X + (int64_t)gj * ldx;
-                        for (int k = 0; k < d; ++k) {
-                            const double sc = k < ITMAX ? itau[k] : itau_of(k);
-                            const double df = xa[k] * sc - xc[k] * sc;
-                            s = fma(df, df, s);
-                        }
-                    }
+                for (int r = 0; r < 4; ++r) {
+                    const int li = ro + 16 * p + kq + 4 * r, lj = co + 16 * q + r16;
+                    const int gi = si * 128 + li, gj = sj * 128 + lj;
+                    const double ni = nrm[0][li], nj = nrm[1][lj];
+                    const double s = ni + nj - 2.0 * acc[p][q][r];
+                    acc[p][q][r] = s;
+                    if (s < 0.5 * (ni + nj) && gi != gj && gi < n && gj < n)
+                        fix |= 1ull << (16 * p + 4 * q + r);
                 }
-                double val;
-                if (gi < n && gj < n)
-                    val = (gi == gj) ? sigma + eps : sigma * exp(-0.5 * s);
-                else
-                    val = (gi == gj) ? 1.0 : 0.0;
-                acc[p][q][r] = val;
+        // (2) those pairs in the direct form, one per lane and iteration (rolled: a 64-way
+        // select puts the value in place; the inlined per-pair form overflowed the instruction
+        // cache, a call per pair spilled the accumulators)
+        while (fix) {
+            const int e = __builtin_ctzll(fix);
+            fix &= fix - 1;
+            const int p = e >> 4, q = (e >> 2) & 3, r = e & 3;
+            const int li = ro + 16 * p + kq + 4 * r, lj = co + 16 * q + r16;
+            double sf = 0.0;
+            if (d <= GK) {
+                for (int k = 0; k < d; ++k) {
+                    const double df = zi[k][li] - zj[k][lj];
+                    sf = fma(df, df, sf);
+                }
+            } else {
+                const double* xa = X + (int64_t)(si * 128 + li) * ldx;
+                const double* xc = X + (int64_t)(sj * 128 + lj) * ldx;
+                for (int k = 0; k < d; ++k) {
+                    const double t = k < ITMAX ? itau[k] : itau_of(k);
+                    const double df = xa[k] * t - xc[k] * t;
+                    sf = fma(df, df, sf);
+                }
             }
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                        if (16 * pp + 4 * qq + rr == e) acc[pp][qq][rr] = sf;
+        }
+        // (3) K
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = si * 128 + ro + 16 * p + kq + 4 * r;
+                    const int gj = sj * 128 + co + 16 * q + r16;
+                    const double s = acc[p][q][r];
+                    double val;
+                    if (gi < n && gj < n)
+                        val = (gi == gj) ? sigma + eps
+                                         : (GRAM_ABL == 1 ? sigma * s : sigma * exp(-0.5 * s));
+                    else
+                        val = (gi == gj) ? 1.0 : 0.0;
+                    acc[p][q][r] = val;
+                }
+    }
+    if (si == sj) {
+        // Diagonal tiles (waves 0 and 3 of a diagonal super-tile): the entries above the
+        // diagonal take the values of their mirror images below it, so that K is exactly
+        // symmetric as the reference's (kernels.pyx fills K[i,j] and K[j,i] with one value; the
+        // f64 MFMA need not give G_ij and G_ji bit for bit). Through the no longer needed LDS
+        // chunks (wave 0: zi, wave 3: zj, 64 x 65 doubles each), after every wave's fix-ups.
+        __syncthreads();
+        if (mine && ti == tj) {
+            double* Tm = wv == 0 ? &zi[0][0] : &zj[0][0];
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        Tm[(16 * p + kq + 4 * r) * 65 + 16 * q + r16] = acc[p][q][r];
+            // (one wave writes and reads its own region: LDS operations of a wave are ordered)
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = p; q < 4; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int li = 16 * p + kq + 4 * r, lj = 16 * q + r16;
+                        if (li < lj) acc[p][q][r] = Tm[lj * 65 + li];
+                    }
+        }
+    }
+    if (!mine) return;
+    if (GRAM_ABL == 2 && acc[0][0][0] != -1.0) return;
     auto store = [&](double* base, int64_t ld) {
 #pragma unroll
         for (int p = 0; p < 4; ++p)

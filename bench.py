@@ -686,22 +686,34 @@ def main():
     gms, gcnt, gbytes = prof['gram']
     if gcnt:
         ach = gbytes / (gms * 1e-3) / 1e12
-        tr, src = pmc_traffic('k_gram')
+        tr, src = pmc_traffic('k_gram_mfma', 'k_gram')
+        # the compute side: pairs per launch from the algorithmic bytes (8 (N D + N (N+1) / 2)
+        # per chain), 2 D flops per pair for z_i . z_j on the f64 MFMA (k_gram_mfma)
+        per_chain = 8.0 * (a.n * a.d + 0.5 * a.n * (a.n + 1))
+        pairs = (gbytes / gcnt) / per_chain * 0.5 * a.n * (a.n + 1)
+        dist_tf = 2.0 * a.d * pairs / (gms * 1e-3 / gcnt) / 1e12
         extra['roofline_gram'] = {'bound': 'hbm', 'achieved': ach, 'peak': PEAK_HBM_TBS,
                                   'unit': 'TB/s', 'frac': ach / PEAK_HBM_TBS, 'traffic': tr,
                                   'traffic_source': src,
                                   'launches': gcnt, 'avg_launch_us': gms * 1e3 / gcnt,
-                                  'algorithmic_bytes_per_launch': gbytes / gcnt}
+                                  'algorithmic_bytes_per_launch': gbytes / gcnt,
+                                  'compute': {'distance_tflops': dist_tf,
+                                              'frac_f64_peak': dist_tf / PEAK_F64_MFMA_TFLOPS,
+                                              'note': 'z_i.z_j on the f64 MFMA (2 D flops per '
+                                                      'pair; MI355X fp64 vector and matrix peaks '
+                                                      'are both 78.6 TFLOP/s) plus one fp64 exp '
+                                                      'per pair on the VALU'}}
     ums, ucnt, uflops = prof['ugemm']
     if ucnt:
         ach = uflops / (ums * 1e-3) / 1e12
-        tr, src = pmc_traffic('k_ugemm')
+        lu_names = ('k_ugemm<1>', 'k_ugemm<2>', 'k_ugemm')  # (round-3 name: untemplated)
+        tr, src = pmc_traffic(*lu_names)
         extra['roofline_lu'] = {'bound': 'mfma', 'achieved': ach, 'peak': PEAK_F32_MFMA_TFLOPS,
                                 'unit': 'TFLOP/s', 'frac': ach / PEAK_F32_MFMA_TFLOPS,
                                 'traffic': tr, 'traffic_source': src, 'launches': ucnt,
                                 'avg_launch_us': ums * 1e3 / ucnt,
                                 'algorithmic_flops_per_launch': uflops / ucnt}
-        mf = pmc_mfma('f32', 'k_ugemm')
+        mf = pmc_mfma('f32', *lu_names)
         if mf:
             extra['roofline_lu']['mfma_busy'] = mf
 

@@ -1,12 +1,10 @@
 set -e
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 60 ./tools/gram.bin > gpurun_out/gram.txt 2>&1
-timeout -k 10 60 ./tools/gram.bin 64 64 >> gpurun_out/gram.txt 2>&1
-timeout -k 10 60 ./tools/gram.bin 64 8 >> gpurun_out/gram.txt 2>&1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "gram or cache_tuple or golden" > gpurun_out/t_gram.txt 2>&1
-for L in new w2 old new w2 old; do
-  unset APM_LIB APM_UGEMM_W2_MIN
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+for L in new old new old; do
+  unset APM_LIB
   if [ $L = old ]; then export APM_LIB=$PWD/tools/_oldlib/libapm.so; fi
-  if [ $L = w2 ]; then export APM_UGEMM_W2_MIN=1; fi
-  timeout -k 10 120 python -u tools/ugemm_bench.py --batches 1,4,8,21,64 --reps 20 2>&1 | sed "s/^/$L /" >> gpurun_out/ugemm_ab.txt
+  timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/ab_$L.json 2> gpurun_out/ab.err
+  python3 -c "import json;d=json.load(open('gpurun_out/ab_$L.json'));print('$L', round(d['value'],2), d['parity']['pass'], round(d['roofline_lu']['avg_launch_us'],1), round(d['roofline_lu']['frac'],3), d['wall_split_s'])"
 done
