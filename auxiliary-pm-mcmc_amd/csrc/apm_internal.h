@@ -80,7 +80,7 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
 // tile columns [K, K+ncols) of an outer panel (diagonal tile (K, K) already factored) in one
 // dataflow launch (chol32.hip: per-(chain, row) progress words prog[b * pstride + row], monotonic
 // base per factorisation and panel)
-void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
+bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base,
                             unsigned long long* timeouts, hipStream_t s);

@@ -428,12 +428,13 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
-            if (Kend - K > 14) throw HipError{"dataflow Newton panel wider than 14 tiles"};
-            launch_chol_panel_df32(M, K, Kend - K, R,
-                                   FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
-                                   count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
-                                   (fact << 16) | ((unsigned long long)(K / OUTER32) << 4),
-                                   c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream);
+            if (!launch_chol_panel_df32(M, K, Kend - K, R,
+                                        FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code},
+                                        lv, count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog,
+                                        c->nb + 1,
+                                        (fact << 16) | ((unsigned long long)(K / OUTER32) << 4),
+                                        c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream))
+                throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
             have_diag = Kend < k1;
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,

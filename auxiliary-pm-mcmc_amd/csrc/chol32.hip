@@ -580,15 +580,18 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
     }
 }
 
-void launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
+bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base,
                             unsigned long long* timeouts, hipStream_t s) {
-    // ncols <= 14 is the caller's contract (chol_range32 throws before launching wider panels)
-    if (ncols < 1 || R - K <= 1) return;  // (one column: its panel TRSM)
+    // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
+    // caller raises) instead of being left unfactored
+    if (ncols > 14) return false;
+    if (ncols < 1 || R - K <= 1) return true;  // (one column: its panel TRSM)
     const long total = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32, dim3((unsigned)total), dim3(256), 0, s, A, K, ncols,
                        nchains, fd, live, hlim, h3ok, prog, pstride, base, timeouts);
+    return true;
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
