@@ -369,7 +369,17 @@ __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float*
 #ifndef DF_WPE
 #define DF_WPE 2  // min workgroups per CU of the dataflow panel kernel
 #endif
-__global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
+#ifndef DF_BULK_WPE
+#define DF_BULK_WPE 3  // ... and of its bulk-row twin (no diagonal factorisation, no waits)
+#endif
+// BULK = false: rows [K, Kend + ...) as described above (with the split launch: rows [K, Kend)
+// only, the diagonal block). BULK = true: the rows below the diagonal block, [Kend, R), after
+// the diagonal block's launch: the same row walk (same operands, same accumulation order: bitwise
+// the same tiles) without the waits - every diagonal tile is final - and without the diagonal
+// factorisation code, whose registers held the combined kernel at 2 workgroups per CU while the
+// bulk rows' walks (~13 us per column, latency-bound) are throughput-limited by residency.
+template <bool BULK>
+__global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
                                                          FusedDiag<float> fd, Live live, int hlim,
                                                          const int* __restrict__ h3ok,
                                                          unsigned long long* prog,
@@ -383,9 +393,9 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
     } sm;
     __shared__ unsigned long long seen;
     const int b = (int)(blockIdx.x % nchains);
-    const int i = K + (int)(blockIdx.x / nchains);
     const int Kend = K + ncols;
-    const bool pub = i < Kend;  // rows of the diagonal block: later rows wait on them
+    const int i = (BULK ? Kend : K) + (int)(blockIdx.x / nchains);
+    const bool pub = !BULK && i < Kend;  // rows of the diagonal block: later rows wait on them
     unsigned long long* pr = prog + b * pstride;
     auto publish = [&](unsigned long long v) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores drained
@@ -446,7 +456,9 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
         if (c > 0) {  // left-looking update by the panel's earlier columns (k_chol_update32)
-            if (i != k) {
+            if (BULK) {
+                // (every diagonal-block tile is final: written by the launch before)
+            } else if (i != k) {
                 if (!wait_row(k, base + c)) {
                     leave_failed();
                     return;
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
                 }
                 __syncthreads();
             }
-            if (i == k) {  // the diagonal tile: its last column's slices and the old tile
+            if (!BULK && i == k) {  // the diagonal tile: its last column's slices and the old tile
 #pragma unroll
                 for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -479,7 +491,7 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
                                      Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c, sm.g,
                                      Aik, A.ld);
             }
-            if (k + 1 == i) {  // next step is the diagonal tile: its columns K .. k-1 now
+            if (!BULK && k + 1 == i) {  // next step is the diagonal tile: its columns K .. k-1 now
                 if (h3)
                     tile_gemm_nt32<true, true>(dacc, Ai + K * 64, A.ld, Ai + K * 64, A.ld, 64 * c,
                                                sm.g, nullptr, 0);
@@ -491,7 +503,7 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
             tile32_load(acc, Aik, A.ld, wr, wc, lane);
         }
         DF_STAMP(2);
-        if (i == k) {  // diagonal tile: factor and publish (row i is then done)
+        if constexpr (!BULK) if (i == k) {  // diagonal tile: factor and publish (row i is then done)
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -530,7 +542,7 @@ __global__ __launch_bounds__(256, DF_WPE) void k_chol_panel_df32(MatF A, int K, 
                     sm.g.a[wc][32 * wr + 16 * bi + F32_CROW(lane, r)][16 * bj + (lane & 15)] =
                         acc[bi][bj][r];
         // inv(L_KK) comes from the launch before; later columns' from row k's workgroup
-        if (c > 0 && !wait_row(k, base + c + 1)) {
+        if (!BULK && c > 0 && !wait_row(k, base + c + 1)) {
             leave_failed();
             return;
         }
@@ -588,9 +600,20 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
     // caller raises) instead of being left unfactored
     if (ncols > 14) return false;
     if (ncols < 1 || R - K <= 1) return true;  // (one column: its panel TRSM)
-    const long total = (long)(R - K) * nchains;
-    hipLaunchKernelGGL(k_chol_panel_df32, dim3((unsigned)total), dim3(256), 0, s, A, K, ncols,
-                       nchains, fd, live, hlim, h3ok, prog, pstride, base, timeouts);
+    static int split = -1;  // APM_DF_SPLIT=0: one launch for all rows (bitwise the same tiles)
+    if (split < 0) {
+        const char* e = getenv("APM_DF_SPLIT");
+        split = e ? atoi(e) != 0 : 0;
+    }
+    const int Kend = K + ncols;
+    const int rows1 = split ? std::min(R, Kend) - K : R - K;
+    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)rows1 * nchains)), dim3(256),
+                       0, s, A, K, ncols, nchains, fd, live, hlim, h3ok, prog, pstride, base,
+                       timeouts);
+    if (split && R > Kend)
+        hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - Kend) * nchains)),
+                           dim3(256), 0, s, A, K, ncols, nchains, fd, live, hlim, h3ok, prog,
+                           pstride, base, timeouts);
     return true;
 }
 
