@@ -379,7 +379,7 @@ __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float*
 // factorisation code, whose registers held the combined kernel at 2 workgroups per CU while the
 // bulk rows' walks (~13 us per column, latency-bound) are throughput-limited by residency.
 template <bool BULK>
-__global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int nchains,
+__global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int R, int nchains,
                                                          FusedDiag<float> fd, Live live, int hlim,
                                                          const int* __restrict__ h3ok,
                                                          unsigned long long* prog,
@@ -392,9 +392,22 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
         DiagSmem32 d;
     } sm;
     __shared__ unsigned long long seen;
-    const int b = (int)(blockIdx.x % nchains);
     const int Kend = K + ncols;
-    const int i = (BULK ? Kend : K) + (int)(blockIdx.x / nchains);
+    int b, i;
+    if constexpr (BULK) {
+        // no dependencies between these workgroups: XCD-aware and chain-major (dispatch slot s
+        // runs on XCD s % 8, which takes a contiguous range of chains), so that the workgroups
+        // sharing a chain's diagonal-block tiles share an L2 and few chains' panels are live in
+        // the Infinity Cache at a time
+        const long rows = R - Kend, total = rows * nchains, L = blockIdx.x;
+        const long xcd = L & 7, q = total >> 3, rm = total & 7;
+        const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
+        b = (int)(item / rows);
+        i = Kend + (int)(item % rows);
+    } else {
+        b = (int)(blockIdx.x % nchains);
+        i = K + (int)(blockIdx.x / nchains);
+    }
     const bool pub = !BULK && i < Kend;  // rows of the diagonal block: later rows wait on them
     unsigned long long* pr = prog + b * pstride;
     auto publish = [&](unsigned long long v) {
@@ -608,11 +621,11 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
     const int Kend = K + ncols;
     const int rows1 = split ? std::min(R, Kend) - K : R - K;
     hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)rows1 * nchains)), dim3(256),
-                       0, s, A, K, ncols, nchains, fd, live, hlim, h3ok, prog, pstride, base,
+                       0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base,
                        timeouts);
     if (split && R > Kend)
         hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - Kend) * nchains)),
-                           dim3(256), 0, s, A, K, ncols, nchains, fd, live, hlim, h3ok, prog,
+                           dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog,
                            pstride, base, timeouts);
     return true;
 }
