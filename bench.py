@@ -688,10 +688,11 @@ def main():
         ach = gbytes / (gms * 1e-3) / 1e12
         tr, src = pmc_traffic('k_gram_mfma', 'k_gram')
         # the compute side: pairs per launch from the algorithmic bytes (8 (N D + N (N+1) / 2)
-        # per chain), 2 D flops per pair for z_i . z_j on the f64 MFMA (k_gram_mfma)
+        # per chain); the direct form (k_gram, the default) spends a subtract and an fma, 3 fp64
+        # flops, per pair and feature on the VALU
         per_chain = 8.0 * (a.n * a.d + 0.5 * a.n * (a.n + 1))
         pairs = (gbytes / gcnt) / per_chain * 0.5 * a.n * (a.n + 1)
-        dist_tf = 2.0 * a.d * pairs / (gms * 1e-3 / gcnt) / 1e12
+        dist_tf = 3.0 * a.d * pairs / (gms * 1e-3 / gcnt) / 1e12
         extra['roofline_gram'] = {'bound': 'hbm', 'achieved': ach, 'peak': PEAK_HBM_TBS,
                                   'unit': 'TB/s', 'frac': ach / PEAK_HBM_TBS, 'traffic': tr,
                                   'traffic_source': src,
@@ -699,10 +700,12 @@ def main():
                                   'algorithmic_bytes_per_launch': gbytes / gcnt,
                                   'compute': {'distance_tflops': dist_tf,
                                               'frac_f64_peak': dist_tf / PEAK_F64_MFMA_TFLOPS,
-                                              'note': 'z_i.z_j on the f64 MFMA (2 D flops per '
-                                                      'pair; MI355X fp64 vector and matrix peaks '
-                                                      'are both 78.6 TFLOP/s) plus one fp64 exp '
-                                                      'per pair on the VALU'}}
+                                              'note': 'direct form sum_k (z_ik - z_jk)^2 on '
+                                                      'the fp64 VALU (3 D flops per pair; the '
+                                                      'MI355X fp64 vector peak is 78.6 TFLOP/s) '
+                                                      'plus one fp64 exp per pair; the GEMM form '
+                                                      'on the f64 MFMA is APM_GRAM_MFMA=1 '
+                                                      '(DESIGN.md §5)'}}
     ums, ucnt, uflops = prof['ugemm']
     if ucnt:
         ach = uflops / (ums * 1e-3) / 1e12
