@@ -1,8 +1,6 @@
 set -e
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-APM_DF_SPLIT=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "dataflow or mixed or fp16x3" > gpurun_out/t_df.txt 2>&1 || { tail -30 gpurun_out/t_df.txt; exit 1; }
-tail -1 gpurun_out/t_df.txt
-bash tools/phases.sh APM_DF_SPLIT 1 0 > gpurun_out/ph.txt 2>&1
-grep -E "^==|^hash|theta-call wall|newton \(|panel_df" gpurun_out/ph.txt
-APM_LIB=$PWD/tools/_wpe2/libapm.so bash tools/phases.sh APM_DF_SPLIT 1 > gpurun_out/ph2.txt 2>&1
-echo "wpe2:"; grep -E "^==|^hash|theta-call wall|newton \(|panel_df" gpurun_out/ph2.txt
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_knobs.py -x -v --timeout 500 --timeout-method thread > gpurun_out/t_knobs.txt 2>&1 || { tail -30 gpurun_out/t_knobs.txt; exit 1; }
+tail -3 gpurun_out/t_knobs.txt
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench20.json 2> gpurun_out/bench20.err
+python3 -c "import json;d=json.loads(open('gpurun_out/bench20.json').read().strip().splitlines()[-1]);print(d['value'], d['parity']['pass'], d['pmc_provenance']['stale'], d['ess_per_sec'])"
