@@ -32,6 +32,6 @@ try:
             L, f = ctx.slot_read(b)[:2]
             h.update(np.ascontiguousarray(f).tobytes())
             h.update(np.ascontiguousarray(L).tobytes())
-    print('digest', h.hexdigest(), 'status', list(st1), 'nops', list(nops))
+    print('digest', h.hexdigest(), 'status', [int(v) for v in st1], 'nops', [int(v) for v in nops])
 finally:
     ctx.close()
