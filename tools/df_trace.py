@@ -43,3 +43,23 @@ for k in range(1, 8):
         us(nx[4]) if nx is not None else -1, us(nn[2]) if nn is not None else -1))
 print('bulk row 40: ' + ' '.join('{0:.1f}/{1:.1f}'.format(us(T[40, c, 3]), us(T[40, c, 2]))
                                  for c in range(8)))
+# bulk rows (below the diagonal block) of the same panel: when each row's walk starts, and per
+# column step the update (start -> update end) and the TRSM (update end -> stored) times
+rows = [r for r in range(8, 64) if T[r, 0, 0] > 0]
+if rows:
+    st = np.array([us(T[r, 0, 0]) for r in rows])
+    print('bulk rows traced: {0}, walk start min/median/max {1:.1f} / {2:.1f} / {3:.1f} us'.format(
+        len(rows), st.min(), np.median(st), st.max()))
+    upd = np.array([[us(T[r, c, 2]) - us(T[r, c, 0]) for c in range(8)] for r in rows])
+    # TRSM + store: update end -> the next column's step start (bulk rows stamp no event 4)
+    trs = np.array([[us(T[r, c + 1, 0]) - us(T[r, c, 2]) for c in range(7)] for r in rows])
+    wait = np.array([[us(T[r, c, 1]) - us(T[r, c, 0]) if T[r, c, 1] > 0 else 0.0
+                      for c in range(8)] for r in rows])
+    end = np.array([us(T[r, 7, 2]) for r in rows])
+    print('per column (median over rows): wait-for-chain ' +
+          ' '.join('%.1f' % v for v in np.median(wait, 0)))
+    print('                              update (incl. wait) ' +
+          ' '.join('%.1f' % v for v in np.median(upd, 0)))
+    print('                              trsm ' + ' '.join('%.1f' % v for v in np.median(trs, 0)))
+    print('last update end min/median/max {0:.1f} / {1:.1f} / {2:.1f} us'.format(
+        end.min(), np.median(end), end.max()))
