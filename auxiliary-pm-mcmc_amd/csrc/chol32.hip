@@ -192,152 +192,6 @@ __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* _
     }
 }
 
-// The same product for TWO vertically adjacent 64x64 tiles (A: 128 rows) against one B: the B
-// slice is staged once for both. Per output tile the MFMA sequence is tile_gemm_nt32's (same
-// slices, same order, same fp16x3 splits), so the tiles are bitwise those of two calls.
-struct GemmSmem32x2 {
-    union {
-        struct {
-            float a[2][128][LP32];
-            float b[2][64][LP32];
-        };
-        struct {
-            _Float16 ah[2][128][LPH], al[2][128][LPH];
-            _Float16 bh[2][64][LPH], bl[2][64][LPH];
-        };
-    };
-};
-template <bool NEG, bool H3>
-__device__ __forceinline__ void tile_gemm_nt32_r2(f4_t (&acc)[2][2][2], const float* __restrict__ A,
-                                                  int64_t lda, const float* __restrict__ B,
-                                                  int64_t ldb, int depth, GemmSmem32x2& sm,
-                                                  const float* __restrict__ C, int64_t ldc) {
-    constexpr int PPR = KS32 / 4;
-    constexpr int PA = 128 * PPR / 256, PB = 64 * PPR / 256;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w >> 1, wc = w & 1;
-    const int r16 = lane & 15, kq = lane >> 4;
-    auto gload = [&](int sidx, f4_t (&ra)[PA], f4_t (&rb)[PB]) {
-#pragma unroll
-        for (int h = 0; h < PA; ++h) {
-            const int p = tid + 256 * h;
-            ra[h] = *reinterpret_cast<const f4_t*>(A + (int64_t)(p / PPR) * lda + sidx * KS32 +
-                                                   (p % PPR) * 4);
-        }
-#pragma unroll
-        for (int h = 0; h < PB; ++h) {
-            const int p = tid + 256 * h;
-            rb[h] = *reinterpret_cast<const f4_t*>(B + (int64_t)(p / PPR) * ldb + sidx * KS32 +
-                                                   (p % PPR) * 4);
-        }
-    };
-    auto sstore = [&](int buf, const f4_t (&ra)[PA], const f4_t (&rb)[PB]) {
-#pragma unroll
-        for (int h = 0; h < PA; ++h) {
-            const int p = tid + 256 * h, row = p / PPR, col = (p % PPR) * 4;
-            if constexpr (H3) {
-                h4_t hi, lo;
-                split_h3(NEG ? -ra[h] : ra[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.ah[buf][row][col]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.al[buf][row][col]) = lo;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sm.a[buf][row][col + e] = NEG ? -ra[h][e] : ra[h][e];
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < PB; ++h) {
-            const int p = tid + 256 * h, row = p / PPR, col = (p % PPR) * 4;
-            if constexpr (H3) {
-                h4_t hi, lo;
-                split_h3(rb[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.bh[buf][row][col]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.bl[buf][row][col]) = lo;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sm.b[buf][row][col + e] = rb[h][e];
-            }
-        }
-    };
-    auto compute = [&](int cur) {
-        if constexpr (H3) {
-            h8_t bh[2], bl[2];
-#pragma unroll
-            for (int x = 0; x < 2; ++x) {
-                bh[x] = *reinterpret_cast<const h8_t*>(&sm.bh[cur][32 * wc + 16 * x + r16][8 * kq]);
-                bl[x] = *reinterpret_cast<const h8_t*>(&sm.bl[cur][32 * wc + 16 * x + r16][8 * kq]);
-            }
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                h8_t ah[2], al[2];
-#pragma unroll
-                for (int x = 0; x < 2; ++x) {
-                    ah[x] = *reinterpret_cast<const h8_t*>(
-                        &sm.ah[cur][64 * t + 32 * wr + 16 * x + r16][8 * kq]);
-                    al[x] = *reinterpret_cast<const h8_t*>(
-                        &sm.al[cur][64 * t + 32 * wr + 16 * x + r16][8 * kq]);
-                }
-#pragma unroll
-                for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                    for (int bj = 0; bj < 2; ++bj) {
-                        acc[t][bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                            ah[bi], bh[bj], acc[t][bi][bj], 0, 0, 0);
-                        acc[t][bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                            ah[bi], bl[bj], acc[t][bi][bj], 0, 0, 0);
-                        acc[t][bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                            al[bi], bh[bj], acc[t][bi][bj], 0, 0, 0);
-                    }
-            }
-            return;
-        }
-#pragma unroll
-        for (int k4 = 0; k4 < KS32 / 4; ++k4) {
-            float b[2];
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj) b[bj] = sm.b[cur][32 * wc + 16 * bj + r16][4 * k4 + kq];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                float a[2];
-#pragma unroll
-                for (int bi = 0; bi < 2; ++bi)
-                    a[bi] = sm.a[cur][64 * t + 32 * wr + 16 * bi + r16][4 * k4 + kq];
-#pragma unroll
-                for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                    for (int bj = 0; bj < 2; ++bj)
-                        acc[t][bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], b[bj],
-                                                                             acc[t][bi][bj], 0, 0, 0);
-            }
-        }
-    };
-    const int nsub = depth / KS32;  // even
-    f4_t ra0[PA], rb0[PB], ra1[PA], rb1[PB];
-    gload(0, ra0, rb0);
-    gload(1, ra1, rb1);
-    sstore(0, ra0, rb0);
-    __syncthreads();
-    for (int s = 0; s < nsub; s += 2) {
-        gload(min(s + 2, nsub - 1), ra0, rb0);
-        compute(0);
-        sstore(1, ra1, rb1);
-        __syncthreads();
-        gload(min(s + 3, nsub - 1), ra1, rb1);
-        compute(1);
-        sstore(0, ra0, rb0);
-        __syncthreads();
-    }
-    // the old tiles, added at the end as in tile_gemm_nt32
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        f4_t old[2][2];
-        tile32_load(old, C + (int64_t)(64 * t) * ldc, ldc, wr, wc, lane);
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj) acc[t][bi][bj] += old[bi][bj];
-    }
-}
-
 // ------------------------------------------------------------------------------- panel, update
 __global__ __launch_bounds__(256) void k_chol_panel32(MatF A, int k, int i0, int glo, int ghi,
                                                       const float* Dinv, int64_t dstride,
@@ -751,114 +605,6 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
     }
 }
 
-// The rows below the diagonal block after the diagonal block's launch (APM_DF_SPLIT=2): as
-// k_chol_panel_df32<true>, but fp16x3 rows in pairs, one workgroup walking two vertically adjacent
-// row tiles through the panel's columns (tile_gemm_nt32_r2: the diagonal-block row's operand
-// staged once for both); the rest (the right-hand-side row, an odd last fp16x3 row) alone.
-// Bitwise the tiles of the row-per-workgroup walks.
-__global__ __launch_bounds__(256, 2) void k_chol_panel_bulk32(MatF A, int K, int ncols, int R,
-                                                              int nchains, FusedDiag<float> fd,
-                                                              Live live, int hlim,
-                                                              const int* __restrict__ h3ok) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
-    __shared__ union {
-        GemmSmem32x2 g2;
-        GemmSmem32 g;
-    } sm;
-    const int Kend = K + ncols;
-    const int H = max(Kend, min(R, hlim));  // rows [Kend, H) may take fp16x3 operands
-    const int P = (H - Kend) / 2;            // pairs
-    const long G = P + (R - Kend - 2 * P);   // row groups per chain
-    const long total = G * nchains, L = blockIdx.x;
-    const long xcd = L & 7, q = total >> 3, rm = total & 7;
-    const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
-    const int b = (int)(item / G), g = (int)(item % G);
-    const bool pair = g < P;
-    const int i = pair ? Kend + 2 * g : Kend + 2 * P + (g - P);
-    if (!live32(live, b)) return;
-    float* Ab = A.base + b * A.cstride;
-    const bool h3 = i < hlim && (!h3ok || h3ok[b]);
-    const float* Ai = Ab + (int64_t)(i * 64) * A.ld;
-    const int nt = pair ? 2 : 1;
-    for (int k = K; k < Kend; ++k) {
-        const int c = k - K;
-        f4_t acc[2][2][2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj) acc[t][bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-        float* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
-        const float* Bk = Ab + (int64_t)(k * 64) * A.ld + K * 64;
-        if (c > 0) {
-            if (pair) {
-                if (h3)
-                    tile_gemm_nt32_r2<true, true>(acc, Ai + K * 64, A.ld, Bk, A.ld, 64 * c, sm.g2,
-                                                  Aik, A.ld);
-                else
-                    tile_gemm_nt32_r2<true, false>(acc, Ai + K * 64, A.ld, Bk, A.ld, 64 * c,
-                                                   sm.g2, Aik, A.ld);
-            } else if (h3) {
-                tile_gemm_nt32<true, true>(acc[0], Ai + K * 64, A.ld, Bk, A.ld, 64 * c, sm.g, Aik,
-                                           A.ld);
-            } else {
-                tile_gemm_nt32<true>(acc[0], Ai + K * 64, A.ld, Bk, A.ld, 64 * c, sm.g, Aik, A.ld);
-            }
-        } else {
-            for (int t = 0; t < nt; ++t)
-                tile32_load(acc[t], Aik + (int64_t)(64 * t) * A.ld, A.ld, wr, wc, lane);
-        }
-        // panel TRSM of each tile: A_ik inv(L_kk)^T (k_chol_panel_df32's staging and product)
-        const float* D = fd.Dinv + b * fd.dstride + (int64_t)k * 4096;
-        for (int t = 0; t < nt; ++t) {
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        sm.g.a[wc][32 * wr + 16 * bi + F32_CROW(lane, r)][16 * bj + (lane & 15)] =
-                            (t == 0 ? acc[0][bi][bj][r] : acc[1][bi][bj][r]);
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int p = threadIdx.x + 256 * h;
-                const int row = p >> 4, col = 4 * (p & 15);
-                const f4_t v = *reinterpret_cast<const f4_t*>(D + row * 64 + col);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sm.g.b[col >> 5][row][(col & 31) + e] = v[e];
-            }
-            __syncthreads();
-            f4_t x[2][2];
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj) x[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-            const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-            for (int cur = 0; cur < 2; ++cur)
-#pragma unroll
-                for (int tt = 0; tt < KS32 / 4; ++tt) {
-                    float a[2], bb[2];
-#pragma unroll
-                    for (int bi = 0; bi < 2; ++bi)
-                        a[bi] = sm.g.a[cur][32 * wr + 16 * bi + r16][4 * tt + kq];
-#pragma unroll
-                    for (int bj = 0; bj < 2; ++bj)
-                        bb[bj] = sm.g.b[cur][32 * wc + 16 * bj + r16][4 * tt + kq];
-#pragma unroll
-                    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                        for (int bj = 0; bj < 2; ++bj)
-                            x[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj],
-                                                                            x[bi][bj], 0, 0, 0);
-                }
-            tile32_store(x, Aik + (int64_t)(64 * t) * A.ld, A.ld, wr, wc, lane);
-            __syncthreads();  // the staging area is reused next
-        }
-    }
-}
-
 bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base,
@@ -870,19 +616,14 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
     static int split = -1;  // APM_DF_SPLIT=0: one launch for all rows (bitwise the same tiles)
     if (split < 0) {
         const char* e = getenv("APM_DF_SPLIT");
-        split = e ? atoi(e) : 0;  // 1: bulk rows one per workgroup; 2: in pairs
+        split = e ? atoi(e) != 0 : 0;
     }
     const int Kend = K + ncols;
     const int rows1 = split ? std::min(R, Kend) - K : R - K;
     hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)rows1 * nchains)), dim3(256),
                        0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base,
                        timeouts);
-    if (split == 2 && R > Kend) {
-        const int H = std::max(Kend, std::min(R, hlim)), P = (H - Kend) / 2;
-        const long G = P + (R - Kend - 2 * P);
-        hipLaunchKernelGGL(k_chol_panel_bulk32, dim3((unsigned)(G * nchains)), dim3(256), 0, s, A, K,
-                           ncols, R, nchains, fd, live, hlim, h3ok);
-    } else if (split && R > Kend)
+    if (split && R > Kend)
         hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - Kend) * nchains)),
                            dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog,
                            pstride, base, timeouts);
