@@ -96,6 +96,11 @@ class _BatchedChains(object):
         # per theta-call: (max, mean) over its chains of the cubic-op count (IS: Newton
         # iterations + 3) - the call's wall time follows the max, its work the mean
         self.call_ops = []
+        # u history for checkpoint / resume (``checkpoint`` / ``restore``): the Philox counter
+        # of the initial draw and, per chain, (counter of nu, cos phi, sin phi) of every
+        # accepted elliptical-slice move — u is a deterministic function of these
+        self.u_init_ctr = np.zeros(C, dtype=np.uint64)
+        self.u_log = [[] for _ in range(C)]
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
@@ -141,9 +146,79 @@ class _BatchedChains(object):
         """u ~ N(0, I) on the device and the first theta-call (reference samplers.py:825-827)."""
         idx = np.arange(self.n_chains)
         self.theta = self.prior_draw() if theta_init is None else np.array(theta_init, float)
+        self.u_init_ctr = self.dev_ctr.copy()
+        self.u_log = [[] for _ in range(self.n_chains)]
         self._normals(idx, self.ub_u)
         self.log_f, self.lp_cur = self._theta_eval(idx, self.theta, self.slot_cur[idx])
         return self.theta.copy()
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def checkpoint(self):
+        """Chain state at a transition boundary as a dict of numpy arrays (``numpy.savez``-able,
+        no pickles): theta, log f, log prior, failure flags, device counters, each chain's
+        RandomState (MT19937 key and position, cached Gaussian) and the u history. u itself
+        (N x N_imp fp64 per chain) is not stored: ``restore`` rebuilds it on the device from
+        the history with the same kernels, bit for bit."""
+        C = self.n_chains
+        keys = np.empty((C, 624), dtype=np.uint32)
+        pos = np.empty(C, dtype=np.int64)
+        has_g = np.empty(C, dtype=np.int64)
+        gauss = np.empty(C)
+        for c, rng in enumerate(self.prngs):
+            _, key, p, hg, g = rng.get_state(legacy=True)
+            keys[c], pos[c], has_g[c], gauss[c] = key, p, hg, g
+        n_log = np.array([len(l) for l in self.u_log], dtype=np.int64)
+        flat = [r for l in self.u_log for r in l]
+        ulog_ctr = np.array([r[0] for r in flat], dtype=np.uint64)
+        ulog_cs = np.array([[r[1], r[2]] for r in flat], dtype=np.float64).reshape(-1, 2)
+        return dict(theta=self.theta.copy(), log_f=self.log_f.copy(), lp_cur=self.lp_cur.copy(),
+                    failed=self.failed.copy(), fail_status=self.fail_status.copy(),
+                    dev_seeds=self.dev_seeds.copy(), dev_ctr=self.dev_ctr.copy(),
+                    rng_key=keys, rng_pos=pos, rng_has_gauss=has_g, rng_gauss=gauss,
+                    u_init_ctr=self.u_init_ctr.copy(), ulog_n=n_log, ulog_ctr=ulog_ctr,
+                    ulog_cs=ulog_cs)
+
+    def restore(self, ck):
+        """Resume from ``checkpoint()`` output (same X, y, chains and seed): host state back,
+        u rebuilt on the device by replaying its draws and accepted moves, then one theta-call
+        at each live chain's current theta refills its cache slot. Returns the largest
+        |log f (recomputed) - log f (saved)| over live chains (0 on a deterministic device)."""
+        C = self.n_chains
+        if not np.array_equal(np.asarray(ck['dev_seeds'], np.uint64), self.dev_seeds):
+            raise ValueError('checkpoint belongs to different chain streams (seed / chains)')
+        self.theta = np.array(ck['theta'], dtype=np.float64)
+        self.failed = np.array(ck['failed'], dtype=bool)
+        self.fail_status = np.array(ck['fail_status'], dtype=np.int32)
+        self.dev_ctr = np.array(ck['dev_ctr'], dtype=np.uint64)
+        for c, rng in enumerate(self.prngs):
+            rng.set_state(('MT19937', np.asarray(ck['rng_key'][c], np.uint32),
+                           int(ck['rng_pos'][c]), int(ck['rng_has_gauss'][c]),
+                           float(ck['rng_gauss'][c])))
+        self.u_init_ctr = np.array(ck['u_init_ctr'], dtype=np.uint64)
+        n_log = np.asarray(ck['ulog_n'], dtype=np.int64)
+        offs = np.r_[0, np.cumsum(n_log)]
+        self.u_log = [[(np.uint64(ck['ulog_ctr'][i]), float(ck['ulog_cs'][i, 0]),
+                        float(ck['ulog_cs'][i, 1])) for i in range(offs[c], offs[c + 1])]
+                      for c in range(C)]
+        idx = np.arange(C)
+        self.ctx.u_normal(self.ub_u[idx], self.dev_seeds[idx], self.u_init_ctr[idx])
+        for k in range(int(n_log.max()) if C else 0):
+            sel = np.flatnonzero(n_log > k)
+            rec = [self.u_log[c][k] for c in sel]
+            self.ctx.u_normal(self.ub_nu[sel], self.dev_seeds[sel],
+                              np.array([r[0] for r in rec], dtype=np.uint64))
+            self.ctx.u_combine(self.ub_prop[sel], self.ub_u[sel], self.ub_nu[sel],
+                               np.array([r[1] for r in rec]), np.array([r[2] for r in rec]))
+            self.ub_u[sel], self.ub_prop[sel] = self.ub_prop[sel].copy(), self.ub_u[sel].copy()
+        live = np.flatnonzero(~self.failed)
+        self.log_f = np.array(ck['log_f'], dtype=np.float64)
+        self.lp_cur = np.array(ck['lp_cur'], dtype=np.float64)
+        if live.size == 0:
+            return 0.
+        saved = self.log_f[live].copy()
+        lf, lp = self._theta_eval(live, self.theta[live], self.slot_cur[live])
+        self.log_f[live], self.lp_cur[live] = lf, lp
+        return float(np.max(np.abs(lf - saved)))
 
     # ------------------------------------------------------------------ updates
     def _ess_u(self, chains=None):
@@ -153,6 +228,7 @@ class _BatchedChains(object):
             np.asarray(chains, dtype=np.int64)[~self.failed[chains]]
         if live.size == 0:
             return
+        nu_ctr = self.dev_ctr.copy()
         self._normals(live, self.ub_nu)
         log_y = np.empty(self.n_chains)
         phi = np.empty(self.n_chains)
@@ -170,8 +246,8 @@ class _BatchedChains(object):
                 self.failed[act] = True
                 break
             t0 = time.perf_counter()
-            self.ctx.u_combine(self.ub_prop[act], self.ub_u[act], self.ub_nu[act],
-                               np.cos(phi[act]), np.sin(phi[act]))
+            cs = np.cos(phi[act]), np.sin(phi[act])
+            self.ctx.u_combine(self.ub_prop[act], self.ub_u[act], self.ub_nu[act], cs[0], cs[1])
             out, st = self.ctx.u_eval(self.slot_cur[act], self.ub_prop[act])
             self.wall['u_call'] += time.perf_counter() - t0
             self.n_u_calls += act.size
@@ -181,6 +257,7 @@ class _BatchedChains(object):
                 if lf[q] > log_y[c]:
                     self.ub_u[c], self.ub_prop[c] = self.ub_prop[c], self.ub_u[c]
                     self.log_f[c] = lf[q]
+                    self.u_log[c].append((nu_ctr[c], float(cs[0][q]), float(cs[1][q])))
                     continue
                 if phi[c] < 0:
                     lo[c] = phi[c]

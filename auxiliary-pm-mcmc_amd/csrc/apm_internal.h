@@ -113,17 +113,12 @@ void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride
                        double* y, int64_t vstride, Live live, int nchains, hipStream_t s);
 void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
                        int64_t vstride, Live live, int nchains, hipStream_t s);
-// the whole solve in one launch (one 1024-thread workgroup per chain), fp64 r -> out (r kept);
-// needs np <= 8192 (trsv32_fused_ok)
-bool trsv32_fused_ok(int np);
-// the same solve over TRM_G workgroups per chain (k_trsv32_mw; NaN-fills `out` first)
+// the whole solve in one launch over TRM_G workgroups per chain (k_trsv32_mw; NaN-fills `out`
+// first; fp64 r -> out, r kept); needs np <= 8192 (trsv32_mw_ok), else the per-block steps above
 bool trsv32_mw_ok(int np);
 void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
                       int fail_code, hipStream_t s);
-void launch_trsv32_fused(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
-                         const double* r, double* out, int64_t vstride, Live live, int nchains,
-                         hipStream_t s);
 // refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
 // acceptance of refinement step `step` on the chains with refining[b] != 0 && status[b] == 0:
 // accepted chains leave the mask; with last = true the others get status = fail_code
@@ -139,12 +134,10 @@ void launch_refine(int mode, const double* Ws, const double* Kb, double* x, cons
 // K[b] (np x np, identity-padded beyond n) from X (n x d, row-major, ldx) and theta[b]
 // kind 0 = isotropic SE (kernels.pyx:12-49), 1 = ARD SE (kernels.pyx:52-90)
 // both: write both triangles (else K's lower tiles only); K2.base: the lower tiles of tile
-// columns < k2cols also to K2; mfma: the GEMM-form distances on the f64 MFMA (k_gram_mfma),
-// else the direct form on the VALU (k_gram)
+// columns < k2cols also to K2 (direct-form distances on the fp64 VALU, k_gram)
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30,
-                 bool mfma = false);
+                 hipStream_t s, bool both, MatB K2 = MatB{nullptr, 0, 0}, int k2cols = 1 << 30);
 
 // ---- newton.hip -----------------------------------------------------------------------------
 struct NewtonVecs {     // all per chain, stride vstride (>= np)
@@ -196,31 +189,11 @@ struct SlotSet {
 // log f by ~1e-10 x trace (11 nats at trace 1.15e11, sigma = e^18.5; < 1e-6 nats at the trace
 // ~1e3 of typical thetas), so this keeps the fp32 rounding of L and U below ~1e-4 nats
 #define APM_WIDE_Q 1.0e6
-// write slot slots[b] from the factored work matrix. mode 0 = IS via the augmented matrix (C_chol
-// at offset (np,np), g in row 2np), mode 1 = PriorMC (K_chol at (0,0), g = 0), mode 2 = IS via
-// chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb)
+// write slot slots[b] from the factored work matrix. mode 1 = PriorMC (K_chol at (0,0), g = 0),
+// mode 2 = IS via chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb)
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s);
-
-extern bool H3DMA;  // chol32.hip: LDS-DMA staging for the fp16x3 trailing update (APM_H3DMA)
-
-// ---- ozaki.hip: fp64 trailing updates emulated exactly on int8 MFMA ---------------------------
-#define OZ_NM 15  // moduli (pairwise coprime, <= 256; log2 of their product 118.57)
-struct OzPlanes {
-    int8_t* base;     // per chain: OZ_NM planes of rows x depth int8 residues
-    int64_t mstride;  // bytes per plane (rows * depth)
-    int64_t cstride;  // bytes per chain
-    int* exps;        // per chain: row scale exponents (row r - row0)
-    int64_t estride;
-    int row0;         // matrix row of plane row 0
-};
-hipError_t oz_init_device();
-int oz_beta(int depth);
-void launch_oz_split(MatB A, int row0, int nrows, int col0, int depth, OzPlanes P, int beta,
-                     Live live, int nchains, hipStream_t s);
-void launch_oz_update_t128(MatB A, OzPlanes P, int depth, const unsigned* tiles, int ntiles,
-                           int plus, Live live, int nchains, hipStream_t s, FusedDiag<double> fd);
 
 // ---- postcov.hip ----------------------------------------------------------------------------
 void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,

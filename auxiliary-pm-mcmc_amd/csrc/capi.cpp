@@ -33,9 +33,12 @@ struct ProfRec {
 struct apm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    bool fuse_diag = true;  // APM_FUSE_DIAG=0: stand-alone diag launches (development knob)
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
+    // tiles per outer panel of the fp64 factorisations (APM_OUTER) and of the Newton matrix
+    // (APM_OUTER32, <= 14: the dataflow panel's progress word packs the column step in 4 bits,
+    // 15 = failed; rhs_row_update32 covers a depth of 16 tiles)
+    int outer = 8, outer32 = 8;
     std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
     std::vector<int> slot_wide;  // host mirror of Sl.wide (read back with each theta-call)
     double eps = 1e-8, tol = 1e-4;
@@ -68,14 +71,12 @@ struct apm_ctx {
     // (APM_EXPORT=0: filled by hipMemcpyAsync instead), dx its device address
     unsigned* hx = nullptr;
     unsigned* dx = nullptr;
-    bool export_rb = true;
     double *d_ca = nullptr, *d_cb = nullptr;
     uint64_t *d_seeds = nullptr, *d_ctrs = nullptr;
     double* U64 = nullptr;
     SlotSet Sl{};
     UPool Up{};
     std::vector<void*> allocs;
-    bool postcov_aug = false;  // APM_POSTCOV=aug: TRSM+SYRK+chol(C) on the augmented matrix
     // K's upper triangle holds valid data (host-uploaded K, or the Gram wrote both triangles);
     // otherwise every K x product uses the symmetric lower-tile kernel (launch_symv)
     bool k_full = false;
@@ -88,22 +89,7 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
-    bool rhs_row = true;  // APM_RHS_ROW=0: the Newton rhs row tile through the 128x128 tile path
-    bool gram2 = true;    // APM_GRAM2=0: K's working copies by k_copy_lower instead of the Gram
-    // APM_GRAM_MFMA=1: the GEMM-form Gram on the f64 MFMA (k_gram_mfma: -8 % kernel time, but
-    // the K of the ill-conditioned sigma = e^18.5 fixture moves its estimate outside twice the
-    // reference's own spread); default: the reference's direct form (k_gram)
-    bool gram_mfma = false;
-    // fp64 outer (rank-64*OUTER) trailing updates on int8 MFMA (ozaki.hip, APM_OZAKI); one
-    // residue-plane buffer per stream (the concurrent chol(K) runs on stream2)
-    bool ozaki = false;
-    OzPlanes ozp[2]{};
-    int64_t oz_rows = 0;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
-    int t128 = 3;
-    bool left_inner = true;
-    bool trsv_fused = true;
-    bool trsv_mw = true;  // APM_TRSV_MW=0: one workgroup per chain (k_trsv32_fused)
     bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
@@ -221,8 +207,6 @@ Exec main_exec(apm_ctx* c) { return Exec{c->stream, live_of(c), c->Dinv, c->ldet
 // rank-256 update per outer panel (4x less read-modify-write traffic than rank-64 steps).
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
-static int OUTER = 8;  // tiles per outer panel (APM_OUTER overrides, development knob)
-static int OUTER32 = 8;  // the same for the Newton factorisation (APM_OUTER32)
 
 // Row tiles [lo, hi) known to be zero in panel column k (skipped by panel and update).
 struct Gap {
@@ -271,9 +255,8 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     const Exec E = ex ? *ex : main_exec(c);
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
-    const bool t128 =
-        (c->t128 & 2) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k));
-    if (src && (!t128 || c->ozaki || plus == 2))  // (theta_eval_impl enables it only where it holds)
+    const bool t128 = kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k));
+    if (src && (!t128 || plus == 2))  // (theta_eval_impl enables it only where it holds)
         throw HipError{"out-of-place update needs the fp64 t128 path"};
     const auto tl = tile_list(c, i0, R, j0, jend, g);
     if (tl.second <= 0) return;
@@ -284,21 +267,8 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE_OUTER : -1, fl, E.s);
     if (t128) {
         const auto sl = super_list(c, i0, R, j0, jend, g);
-        if (c->ozaki && plus != 2 && kc <= OUTER && kc % 4 == 0 &&
-            (int64_t)(R - j0) * 64 <= c->oz_rows) {
-            // rows [j0, R) of the panel's columns -> residue planes, then the int8 update
-            OzPlanes P = c->ozp[E.s == c->stream2 ? 1 : 0];
-            P.row0 = j0 * 64;
-            const int depth = 64 * kc;
-            P.mstride = c->oz_rows * depth;
-            launch_oz_split(M, j0 * 64, (R - j0) * 64, k0 * 64, depth, P, oz_beta(depth), E.lv,
-                            count, E.s);
-            check_launch();
-            launch_oz_update_t128(M, P, depth, sl.first, sl.second, plus, E.lv, count, E.s, fd);
-        } else {
-            launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd,
-                                    src ? *src : MatB{nullptr, 0, 0});
-        }
+        launch_chol_update_t128(M, k0, kc, sl.first, sl.second, plus, E.lv, count, E.s, fd,
+                                src ? *src : MatB{nullptr, 0, 0});
     } else {
         if (plus == 2) throw HipError{"identity-initialised update needs the t128 path"};
         launch_chol_update(M, k0, kc, tl.first, tl.second, plus != 0, E.lv, count, E.s, fd);
@@ -319,11 +289,11 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
                 const Exec* ex = nullptr, const MatB* first_src = nullptr) {
     const Exec E = ex ? *ex : main_exec(c);
     const Live lv = E.lv;
-    const bool fuse = factor_diag && c->fuse_diag && row_start <= k0;
+    const bool fuse = factor_diag && row_start <= k0;
     bool have_diag = false;  // tile (k, k) already factored by the previous update launch
-    for (int K = k0; K < k1; K += OUTER) {
-        const int Kend = std::min(K + OUTER, k1);
-        if (fuse && c->left_inner) {
+    for (int K = k0; K < k1; K += c->outer) {
+        const int Kend = std::min(K + c->outer, k1);
+        if (fuse) {
             // left-looking inside the outer panel: column k receives all of the panel's earlier
             // columns in ONE update (depth (k-K)*64, one read-modify-write of its tiles instead
             // of k-K), whose first tile is the diagonal tile it then factors (fused diag)
@@ -398,10 +368,10 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
     ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
     ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl);
-    if ((c->t128 & 1) && kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
+    if (kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a
-        // row vector (APM_RHS_ROW=0: as a 64-row tile)
-        const int rhs = c->rhs_row && R > c->nb ? c->nb : -1;
+        // row vector (rhs_row_update32)
+        const int rhs = R > c->nb ? c->nb : -1;
         const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
                                   fd, c->h3_now ? c->nb : 0, c->h3ok, rhs);
@@ -418,11 +388,10 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
-    const bool df = c->df32 && c->fuse_diag && c->left_inner;
     const unsigned long long fact = ++c->df_fact;
-    for (int K = k0; K < k1; K += OUTER32) {
-        const int Kend = std::min(K + OUTER32, k1);
-        if (df) {  // the same steps in one dataflow launch per outer panel (chol32.hip)
+    for (int K = k0; K < k1; K += c->outer32) {
+        const int Kend = std::min(K + c->outer32, k1);
+        if (c->df32) {  // the same steps in one dataflow launch per outer panel (chol32.hip)
             if (!have_diag) {
                 launch_chol_diag32(M, K, D, ds, c->ldet, c->lstride, lv, fail_code, count,
                                    c->stream);
@@ -432,7 +401,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                         FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code},
                                         lv, count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog,
                                         c->nb + 1,
-                                        (fact << 16) | ((unsigned long long)(K / OUTER32) << 4),
+                                        (fact << 16) | ((unsigned long long)(K / c->outer32) << 4),
                                         c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream))
                 throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
@@ -441,36 +410,20 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                              fail_code);
             continue;
         }
-        if (c->fuse_diag && c->left_inner) {  // left-looking inside the panel (chol_range)
-            for (int k = K; k < Kend; ++k) {
-                if (k > K)
-                    tracked_update32(c, M, K, k - K, k, R, k, k + 1, count, k, fail_code);
-                else if (!have_diag) {
-                    launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
-                                       c->stream);
-                    check_launch();
-                }
-                launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
-                check_launch();
-            }
-            have_diag = Kend < k1;
-            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
-                             fail_code);
-            continue;
-        }
+        // APM_DF32=0: the launch sequence the dataflow kernel replaces (left-looking inside the
+        // panel, as chol_range; bitwise the same tiles)
         for (int k = K; k < Kend; ++k) {
-            if (!have_diag) {
+            if (k > K)
+                tracked_update32(c, M, K, k - K, k, R, k, k + 1, count, k, fail_code);
+            else if (!have_diag) {
                 launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
                                    c->stream);
                 check_launch();
             }
             launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
             check_launch();
-            have_diag = c->fuse_diag && k + 1 < Kend;
-            tracked_update32(c, M, k, 1, k + 1, R, k + 1, Kend, count, have_diag ? k + 1 : -1,
-                             fail_code);
         }
-        have_diag = c->fuse_diag && Kend < k1;
+        have_diag = Kend < k1;
         tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                          fail_code);
     }
@@ -478,9 +431,9 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
 
 void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
 
-// Read back up to three small per-chain device arrays (after the work enqueued so far on the
-// main stream) and wait: one k_export launch into the mapped host buffer (or one
-// hipMemcpyAsync per array with APM_EXPORT=0), a stream synchronisation, host copies.
+// Read back up to four small per-chain device arrays (after the work enqueued so far on the
+// main stream) and wait: one k_export launch into the mapped host buffer, a stream
+// synchronisation, host copies.
 struct RB {
     const void* src;
     int bytes;
@@ -488,25 +441,17 @@ struct RB {
 };
 void read_back(apm_ctx* c, std::initializer_list<RB> l) {
     Export e{};
-    int k = 0, off = 0;
+    int k = 0;
     for (const RB& r : l) {
-        if (c->export_rb) {
-            e.src[k] = static_cast<const unsigned*>(r.src);
-            e.words[k] = r.bytes / 4;
-        } else {
-            HIPC(hipMemcpyAsync(reinterpret_cast<char*>(c->hx) + off, r.src, r.bytes,
-                                hipMemcpyDeviceToHost, c->stream));
-        }
-        off += r.bytes;
+        e.src[k] = static_cast<const unsigned*>(r.src);
+        e.words[k] = r.bytes / 4;
         ++k;
     }
-    if (c->export_rb) {
-        e.dst = c->dx;
-        launch_export(e, c->stream);
-        check_launch();
-    }
+    e.dst = c->dx;
+    launch_export(e, c->stream);
+    check_launch();
     sync(c);
-    off = 0;
+    int off = 0;
     for (const RB& r : l) {
         std::memcpy(r.host, reinterpret_cast<const char*>(c->hx) + off, r.bytes);
         off += r.bytes;
@@ -567,13 +512,10 @@ void newton_solve32(apm_ctx* c, int count) {
     chol_range32(c, F, 0, nb, nb + 1, nb, APM_STATUS_CHOL_B, count);  // B32 formed with K b
     launch_row32(F, np, np, r1, vs, lv, count, s);  // y0 = L^-1 rhs (fp32)
     check_launch();
-    const bool fused_trsv = c->trsv_fused && trsv32_fused_ok(np);
-    if (fused_trsv) {
+    const bool mw_trsv = trsv32_mw_ok(np);
+    if (mw_trsv) {
         feed_chol_k(c);
-        if (c->trsv_mw)
-            launch_trsv32_mw(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, APM_STATUS_CHOL_B, s);
-        else
-            launch_trsv32_fused(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, s);
+        launch_trsv32_mw(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, APM_STATUS_CHOL_B, s);
         check_launch();
     } else {
         for (int J = nb - 1; J >= 0; --J) {
@@ -598,18 +540,12 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lr, count, s);       // res
         check_launch();
-        if (fused_trsv) {
+        if (mw_trsv) {
             feed_chol_k(c);
-            if (c->trsv_mw)
-                launch_trsv32_mw(true, F, nb, D, ds, r1, r2, vs, lr, count, APM_STATUS_CHOL_B, s);
-            else
-                launch_trsv32_fused(true, F, nb, D, ds, r1, r2, vs, lr, count, s);
+            launch_trsv32_mw(true, F, nb, D, ds, r1, r2, vs, lr, count, APM_STATUS_CHOL_B, s);
             check_launch();
             feed_chol_k(c);
-            if (c->trsv_mw)
-                launch_trsv32_mw(false, F, nb, D, ds, r2, r3, vs, lr, count, APM_STATUS_CHOL_B, s);
-            else
-                launch_trsv32_fused(false, F, nb, D, ds, r2, r3, vs, lr, count, s);
+            launch_trsv32_mw(false, F, nb, D, ds, r2, r3, vs, lr, count, APM_STATUS_CHOL_B, s);
             check_launch();
         } else {
             for (int J = 0; J < nb; ++J) {
@@ -734,15 +670,15 @@ void newton_is(apm_ctx* c, int count, std::vector<int>& st_h) {
     newton(c, count, st_h, false, (int)redo.size());
 }
 
-void augmented(apm_ctx* c, int count, bool factor_C) {
+// apm_laplace's covariance C = K - V^T V (lpa.py:111-112) in the bottom-right of A: the
+// augmented matrix [[B,.],[K W^1/2, K]] with the last fp64 Newton factor in its top-left
+void augmented(apm_ctx* c, int count) {
     const Live lv = live_of(c);
     HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
     launch_form_aug(c->K, c->A, c->v, c->np, lv, count, c->stream);
     check_launch();
     const int nb = c->nb, R = 2 * nb + 1, Cb = 2 * nb;
-    // top-left L (and its diagonal-block inverses) are the last Newton factorisation
     chol_range(c, c->A, 0, nb, R, Cb, APM_STATUS_CHOL_B, count, /*factor_diag=*/false, /*rows>=*/nb);
-    if (factor_C) chol_range(c, c->A, nb, 2 * nb, R, Cb, APM_STATUS_CHOL_C, count);
 }
 
 // Posterior-covariance factor through chol(K) (postcov.hip): 4N^3/3 flops instead of the
@@ -761,9 +697,9 @@ void chol_k_panel(apm_ctx* c, const Exec& ex) {
     if (K < 0 || K >= c->nb) return;
     // first panel after a partial Gram copy: the trailing update reads K's tiles (out of place)
     const MatB* src = (K == 0 && c->cholk_partial) ? &c->K : nullptr;
-    chol_range(c, bl_of(c), K, std::min(K + OUTER, c->nb), c->nb, c->nb, APM_STATUS_CHOL_K,
+    chol_range(c, bl_of(c), K, std::min(K + c->outer, c->nb), c->nb, c->nb, APM_STATUS_CHOL_K,
                c->cholk_count, true, 0, no_gap, &ex, src);
-    c->cholk_next = K + OUTER;
+    c->cholk_next = K + c->outer;
 }
 void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true, bool partial = false) {
     HIPC(hipMemsetD32Async(c->active2, 1, count, ex.s));
@@ -831,7 +767,7 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     // J M J = I + Y2 Y2^T: on the 128x128 super-tile path one launch writes it without reading TL
     // (tile column j takes Y2's column blocks k <= j); otherwise TL starts as I and receives
     // panel-wide updates (Y2 lower: j >= K suffices)
-    const bool syrk1 = (c->t128 & 2) && nb >= 2;
+    const bool syrk1 = nb >= 2;
     launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s, !syrk1);  // Y2, Y = L_K J
     check_launch();
     if (syrk1) {
@@ -839,8 +775,8 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     } else {
         launch_identity_lower(TL, np, lv, count, s);
         check_launch();
-        for (int K = 0; K < nb; K += OUTER) {
-            const int Kend = std::min(K + OUTER, nb);
+        for (int K = 0; K < nb; K += c->outer) {
+            const int Kend = std::min(K + c->outer, nb);
             tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, 1, count);
         }
     }
@@ -858,12 +794,12 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
     // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
-    const bool ov = est == APM_EST_IS && !c->postcov_aug && c->mixed && c->overlap_k;
+    const bool ov = est == APM_EST_IS && c->mixed && c->overlap_k;
     // the matrix a factorisation of K starts from (chol(K)'s working copy BL, or PriorMC's A):
-    // the Gram writes K's lower tiles there too instead of a later copy pass (APM_GRAM2=0: copy)
+    // the Gram writes K's lower tiles there too instead of a later copy pass
     MatB k2{nullptr, 0, 0};
     int k2cols = 1 << 30;
-    if (gram && c->gram2 && !c->postcov_aug) {
+    if (gram) {
         if (est == APM_EST_PRIORMC) {
             k2 = c->A;
         } else if (ov) {
@@ -871,17 +807,17 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             // chol(K)'s first trailing update can read its old tiles from K (out of place): the
             // Gram then copies only the first outer panel's tile columns (~1/4 of the lower tiles
             // at N = 4096 instead of all of them)
-            if ((c->t128 & 2) && !c->ozaki && OUTER >= 2 && c->nb - OUTER >= 2) k2cols = OUTER;
+            if (c->outer >= 2 && c->nb - c->outer >= 2) k2cols = c->outer;
         }
     }
     if (gram) {
-        // the augmented posterior route (APM_POSTCOV=aug) reads K's upper tiles; every other
-        // consumer reads the lower ones: the Gram then writes N(N+1)/2 entries
-        c->k_full = c->postcov_aug;
+        // every consumer on this path reads K's lower tiles: the Gram writes N(N+1)/2 entries
+        // 
+        c->k_full = false;
         const double nk = c->k_full ? (double)c->n * c->n : 0.5 * (double)c->n * (c->n + 1);
         ProfScope ps(c, APM_PROF_GRAM, 8.0 * ((double)c->n * c->d + nk) * count + 8.0 * c->P);
         launch_gram(c->K, c->X, c->d, c->n, c->d, c->theta, c->P, c->kind, c->eps, c->np, lv,
-                    count, c->stream, c->k_full, k2, k2cols, c->gram_mfma);
+                    count, c->stream, c->k_full, k2, k2cols);
         check_launch();
     }
     std::vector<int> st_h(count, 0), it_h(count, 0);
@@ -903,7 +839,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                          /*partial=*/k2cols < c->nb);
         }
         const int64_t reruns = c->n_fp64_rerun;
-        if (est == APM_EST_LAPLACE || c->postcov_aug)  // both use the Newton factor itself
+        if (est == APM_EST_LAPLACE)  // log|B| of the Newton factor itself: fp64 (lpa.py:116)
             newton(c, count, st_h, false, count);
         else
             newton_is(c, count, st_h);
@@ -921,14 +857,8 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                                c->stream);
             check_launch();
         } else {
-            int mode = 2;
-            if (c->postcov_aug) {
-                augmented(c, count, true);
-                mode = 0;
-            } else {
-                post_cov_lk(c, count, ov);
-            }
-            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, mode,
+            post_cov_lk(c, count, ov);
+            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 2,
                               c->n, c->np, lv, count, c->stream);
             check_launch();
             u_eval_device(c, count, true);
@@ -971,38 +901,13 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t ldx, const double* y, double eps, int64_t S, int64_t max_batch,
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
-    if (const char* e = getenv("APM_OUTER")) OUTER = std::max(1, atoi(e));
-    // the Newton panels: <= 14 tiles (the dataflow panel's progress word packs the column step in
-    // 4 bits, 15 = failed; rhs_row_update32 covers a depth of 16 tiles)
-    if (const char* e = getenv("APM_OUTER32")) OUTER32 = std::min(14, std::max(1, atoi(e)));
-    if (const char* e = getenv("APM_POSTCOV")) c->postcov_aug = std::string(e) == "aug";
-    if (const char* e = getenv("APM_SCHED")) {  // host wait policy of synchronisations
-        const std::string m(e);
-        const unsigned f = m == "spin" ? hipDeviceScheduleSpin
-                         : m == "yield" ? hipDeviceScheduleYield
-                         : m == "block" ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
-        (void)hipSetDevice(device);
-        (void)hipSetDeviceFlags(f);  // fails harmlessly once the device is active
-        (void)hipGetLastError();
-    }
+    // development knobs, read here once per context; defaults are the measured best
+    if (const char* e = getenv("APM_OUTER")) c->outer = std::max(1, atoi(e));
+    if (const char* e = getenv("APM_OUTER32")) c->outer32 = std::min(14, std::max(1, atoi(e)));
     HIPC(hipSetDevice(device));
-    if (const char* e = getenv("APM_FUSE_DIAG")) c->fuse_diag = atoi(e) != 0;
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
-    if (const char* e = getenv("APM_EXPORT")) c->export_rb = atoi(e) != 0;
-    if (const char* e = getenv("APM_RHS_ROW")) c->rhs_row = atoi(e) != 0;
-    if (const char* e = getenv("APM_GRAM2")) c->gram2 = atoi(e) != 0;
-    if (const char* e = getenv("APM_GRAM_MFMA")) c->gram_mfma = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
-    if (const char* e = getenv("APM_T128")) c->t128 = atoi(e);
-    if (const char* e = getenv("APM_OZAKI")) c->ozaki = atoi(e) != 0;
-    {  // process-wide kernel choice, re-read at every context creation (default: off)
-        const char* e = getenv("APM_H3DMA");
-        H3DMA = e ? atoi(e) != 0 : false;
-    }
-    if (const char* e = getenv("APM_LEFT")) c->left_inner = atoi(e) != 0;
-    if (const char* e = getenv("APM_TRSV_FUSED")) c->trsv_fused = atoi(e) != 0;
-    if (const char* e = getenv("APM_TRSV_MW")) c->trsv_mw = atoi(e) != 0;
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
@@ -1075,18 +980,6 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, B);
-    if (c->ozaki) {  // residue planes for rows of the largest factorisation (2 np + 64)
-        HIPC(oz_init_device());
-        c->oz_rows = 2 * np + 64;
-        for (int q = 0; q < 2; ++q) {
-            OzPlanes& P = c->ozp[q];
-            P.mstride = c->oz_rows * 64 * OUTER;
-            P.cstride = (int64_t)OZ_NM * P.mstride;
-            P.base = dalloc<int8_t>(c, (size_t)B * P.cstride);
-            P.estride = c->oz_rows;
-            P.exps = dalloc<int>(c, (size_t)B * c->oz_rows);
-        }
-    }
     // + 1: the count of bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS)
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 1);
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 1)));
@@ -1451,10 +1344,8 @@ int apm_gram(int device, int kind, const double* X, int64_t n, int64_t d, int64_
         HIPC(hipMemcpyAsync(c->theta, theta, sizeof(double) * P, hipMemcpyHostToDevice, c->stream));
         HIPC(hipMemsetD32Async(c->active, 1, 1, c->stream));
         HIPC(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
-        // (the cached context's knob, re-read per call: tests compare both kernels)
-        if (const char* e = getenv("APM_GRAM_MFMA")) c->gram_mfma = atoi(e) != 0;
         launch_gram(c->K, c->X, d, (int)n, (int)d, c->theta, P, kind, eps, c->np, live_of(c), 1,
-                    c->stream, true, MatB{nullptr, 0, 0}, 1 << 30, c->gram_mfma);
+                    c->stream, true);
         check_launch();
         HIPC(hipMemcpy2DAsync(K, sizeof(double) * ldk, c->K.base, sizeof(double) * c->np,
                               sizeof(double) * n, n, hipMemcpyDeviceToHost, c->stream));
@@ -1520,7 +1411,7 @@ int apm_laplace(int device, const double* K, int64_t n, int64_t ldk, const doubl
             HIPC(hipMemcpyAsync(lml_out, c->out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
         }
         if (calc_cov) {
-            augmented(c, 1, false);  // bottom-right of A now holds C = K - V^T V (lower)
+            augmented(c, 1);  // bottom-right of A now holds C = K - V^T V (lower)
             std::vector<double> Cb((size_t)np * np);
             HIPC(hipMemcpy2DAsync(Cb.data(), sizeof(double) * np,
                                   c->A.base + (int64_t)np * c->A.ld + np, sizeof(double) * c->A.ld,

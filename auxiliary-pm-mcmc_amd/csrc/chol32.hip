@@ -613,20 +613,9 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
     // caller raises) instead of being left unfactored
     if (ncols > 14) return false;
     if (ncols < 1 || R - K <= 1) return true;  // (one column: its panel TRSM)
-    static int split = -1;  // APM_DF_SPLIT=0: one launch for all rows (bitwise the same tiles)
-    if (split < 0) {
-        const char* e = getenv("APM_DF_SPLIT");
-        split = e ? atoi(e) != 0 : 0;
-    }
-    const int Kend = K + ncols;
-    const int rows1 = split ? std::min(R, Kend) - K : R - K;
-    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)rows1 * nchains)), dim3(256),
+    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)(R - K) * nchains)), dim3(256),
                        0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base,
                        timeouts);
-    if (split && R > Kend)
-        hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - Kend) * nchains)),
-                           dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog,
-                           pstride, base, timeouts);
     return true;
 }
 
@@ -717,11 +706,7 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
         }
     }
 }
-// DMA (with H3): the fp32 operands are staged by LDS-DMA as on the fp32 path and each wave splits
-// the fragments it reads into hi/lo in registers right before its MFMAs (the same split, the same
-// products in the same order: bitwise equal to the register-staged split) - no staging registers,
-// no ds_write pass of four half planes, and the split's VALU work interleaves with the MFMAs.
-template <bool H3, bool DMA = false>
+template <bool H3>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
@@ -776,7 +761,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                 acc[bi][bj][r] = -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
     // super-tile rows below hlim (the appended right-hand side row), chains flagged in h3ok
     const bool use_h3 = H3 && ti + (rv1 ? 1 : 0) < hlim && (!h3ok || h3ok[b]);
-    if (!DMA && use_h3) {
+    if (use_h3) {
         // register staging: thread tid moves 16-byte pieces p = tid + 256h (row p/8, k 4(p%8))
         // of both operands
         const float* arow[4];
@@ -890,42 +875,6 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                                                  (lds_void_t*)&sm.g.b[buf][32 * wv + 8 * q][0], 16, 0, 0);
             }
         };
-        // fp16x3 from the fp32 image: lane (r16, kq) reads pieces 2kq, 2kq+1 (k = 8kq .. 8kq+7,
-        // the v_mfma_f32_16x16x32_f16 fragment) of its rows and splits them in registers
-        auto split8 = [](const f4_t& p0, const f4_t& p1, h8_t& hi, h8_t& lo) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float v = e < 4 ? p0[e] : p1[e - 4];
-                const _Float16 x = (_Float16)v;
-                hi[e] = x;
-                lo[e] = (_Float16)(v - (float)x);
-            }
-        };
-        auto compute_h3 = [&](int cur) {
-            const int s0 = ((2 * kq) ^ (r16 & 7)) * 4, s1 = ((2 * kq + 1) ^ (r16 & 7)) * 4;
-            h8_t bh[4], bl[4];
-#pragma unroll
-            for (int bj = 0; bj < 4; ++bj) {
-                const float* rowp = &sm.g.b[cur][64 * wc + 16 * bj + r16][0];
-                split8(*reinterpret_cast<const f4_t*>(rowp + s0),
-                       *reinterpret_cast<const f4_t*>(rowp + s1), bh[bj], bl[bj]);
-            }
-            h8_t ah[4], al[4];
-#pragma unroll
-            for (int bi = 0; bi < 4; ++bi) {
-                const float* rowp = &sm.g.a[cur][64 * wr + 16 * bi + r16][0];
-                split8(*reinterpret_cast<const f4_t*>(rowp + s0),
-                       *reinterpret_cast<const f4_t*>(rowp + s1), ah[bi], al[bi]);
-            }
-#pragma unroll
-            for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 4; ++bj) {
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-                }
-        };
         // lane group kq takes the slice's k values 8kq .. 8kq+7 (pieces 2kq, 2kq+1; the same k for A
         // and B): a lane's fragments for 4 MFMA steps are one 16-byte LDS read
         auto compute = [&](int cur) {
@@ -952,20 +901,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         glds(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (DMA && use_h3) {  // (uniform per workgroup: one loop per operand precision)
-            for (int s = 0; s < nsub; ++s) {
-                if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);
-                if (mine) compute_h3(s & 1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
-        } else {
-            for (int s = 0; s < nsub; ++s) {
-                if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
-                if (mine) compute(s & 1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
+        for (int s = 0; s < nsub; ++s) {
+            if (s + 1 < nsub) glds(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
+            if (mine) compute(s & 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
         }
     }
 #pragma unroll
@@ -1011,18 +951,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                       tid, 256);
 }
 
-// the LDS-DMA fp16x3 update (APM_H3DMA=1; bitwise equal, measured no faster in situ - DESIGN.md §5)
-bool H3DMA = false;
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
                                int hlim, const int* h3ok, int rhs) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    if (hlim > 0 && H3DMA)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_chol_update32_t128<true, true>), dim3((unsigned)total),
-                           dim3(256), 0, s, A, k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok,
-                           rhs);
-    else if (hlim > 0)
+    if (hlim > 0)
         hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
                            k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs);
     else
@@ -1286,141 +1220,7 @@ __global__ __launch_bounds__(256) void k_trsv_bwd32(MatF A, int J, const float* 
     if (tid < 64) rb[I * 64 + tid] -= part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
 }
 
-// ---------------------------------------------------------------- single-launch TRSV (one WG/chain)
-// The whole solve of one chain in one 1024-thread workgroup, LEFT-looking by 64-row blocks, so no
-// launch per block step and one reduction per step:
-//   FWD  L y = r:    y_J = inv(L_JJ) (r_J - sum_{I<J} L_JI y_I)
-//   BWD  L^T z = r:  z_J = inv(L_JJ)^T (r_J - sum_{I>J} L_IJ^T z_I)
-// Thread t streams the 16-byte pieces (row t/16, columns 4(t%16)..+3) of the tiles of the step
-// (coalesced 256-byte rows), TRF_U tiles of loads in flight, and the first TRF_U tiles (and the
-// inv(L_JJ) piece) of the NEXT step are loaded before this step's reductions, so a step's latency
-// chain (reduce -> barrier -> 64x64 inverse product -> barrier) overlaps the next step's loads.
-// r and the solution so far live in LDS (fp64); partial sums are fp64. FWD row sums reduce over
-// the 16 lanes of a row; BWD column sums over the 64 rows (4 per wave by shuffles, 16 waves through
-// LDS); the inverse product x_J = inv(L_JJ) rj (or its transpose) uses all 1024 threads.
-#define TRF_MAXNP 8192
-#ifndef TRF_U
-#define TRF_U 8  // tiles of loads in flight per thread and step
-#endif
-#define TRF_DP 68  // LDS pitch (floats) of the staged 64x64 inverse
-template <bool FWD>
-__global__ __launch_bounds__(1024) void k_trsv32_fused(MatF A, int nb, const float* Dinv,
-                                                       int64_t dstride, const double* r,
-                                                       double* out, int64_t vstride, Live live) {
-    const int b = blockIdx.x;
-    if (!live32(live, b)) return;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int row = t >> 4, cg = t & 15;
-    extern __shared__ double trf_sm[];
-    double* xs = trf_sm;                                      // np: solution so far
-    double* rs = xs + nb * 64;                                // np: right-hand side
-    double* red = rs + nb * 64;                               // 16 x 64 partials
-    double* rj = red + 16 * 64;                               // 64: right-hand side of the step
-    float* DS = reinterpret_cast<float*>(rj + 64);            // 64 x TRF_DP: inv(L_JJ)
-    const float* Lb = A.base + b * A.cstride;
-    const float* Db = Dinv + b * dstride;
-    for (int i = t; i < nb * 64; i += 1024) rs[i] = r[b * vstride + i];
-    // tile piece (step J, tile I) of this thread
-    auto piece = [&](int J, int I) -> const f4_t* {
-        const int64_t o = FWD ? (int64_t)(J * 64 + row) * A.ld + I * 64 + 4 * cg
-                              : (int64_t)(I * 64 + row) * A.ld + J * 64 + 4 * cg;
-        return reinterpret_cast<const f4_t*>(Lb + o);
-    };
-    auto first = [&](int s) { return FWD ? 0 : nb - s; };  // tiles of step s: [first, first + cnt)
-    f4_t pre[TRF_U];
-    f4_t dv = *reinterpret_cast<const f4_t*>(Db + (int64_t)(FWD ? 0 : nb - 1) * 4096 + row * 64 +
-                                             4 * cg);
-    __syncthreads();
-    for (int s = 0; s < nb; ++s) {
-        const int J = FWD ? s : nb - 1 - s;
-        const int cnt = s;  // FWD: I in [0, J); BWD: I in (J, nb) - both s tiles
-        const int i0 = first(s);
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        auto consume = [&](const f4_t& v, int I) {
-            if (FWD) {
-                const double* x = xs + I * 64 + 4 * cg;
-                acc[0] += (double)v[0] * x[0] + (double)v[1] * x[1] + (double)v[2] * x[2] +
-                          (double)v[3] * x[3];
-            } else {
-                const double x = xs[I * 64 + row];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[q] += (double)v[q] * x;
-            }
-        };
-        // chunk 0 was prefetched during the previous step
-        const int c0 = cnt < TRF_U ? cnt : TRF_U;
-#pragma unroll
-        for (int u = 0; u < TRF_U; ++u)
-            if (u < c0) consume(pre[u], i0 + u);
-        for (int I = i0 + c0; I < i0 + cnt; I += TRF_U) {
-            f4_t v[TRF_U];
-            const int m = min(TRF_U, i0 + cnt - I);
-#pragma unroll
-            for (int u = 0; u < TRF_U; ++u)  // unconditional loads (clamped index): no branches
-                v[u] = *piece(J, min(I + u, i0 + cnt - 1));
-#pragma unroll
-            for (int u = 0; u < TRF_U; ++u)
-                if (u < m) consume(v[u], I + u);
-        }
-        // next step's first chunk and inverse piece, in flight across this step's reductions
-        f4_t dnext = dv;
-        if (s + 1 < nb) {
-            const int Jn = FWD ? s + 1 : nb - 2 - s, in0 = first(s + 1);
-            const int cn = (s + 1) < TRF_U ? (s + 1) : TRF_U;
-#pragma unroll
-            for (int u = 0; u < TRF_U; ++u) pre[u] = *piece(Jn, in0 + min(u, cn - 1));
-            dnext = *reinterpret_cast<const f4_t*>(Db + (int64_t)Jn * 4096 + row * 64 + 4 * cg);
-        }
-        *reinterpret_cast<f4_t*>(DS + row * TRF_DP + 4 * cg) = dv;
-        if (FWD) {  // row sums: 16 lanes per row
-            double sum = acc[0];
-            sum += __shfl_xor(sum, 8, 64);
-            sum += __shfl_xor(sum, 4, 64);
-            sum += __shfl_xor(sum, 2, 64);
-            sum += __shfl_xor(sum, 1, 64);
-            if (cg == 0) rj[row] = rs[J * 64 + row] - sum;
-        } else {  // column sums: the 4 rows of this wave by shuffles, the 16 waves through LDS
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                acc[q] += __shfl_xor(acc[q], 16, 64);
-                acc[q] += __shfl_xor(acc[q], 32, 64);
-            }
-            if (lane < 16) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) red[w * 64 + 4 * cg + q] = acc[q];
-            }
-        }
-        __syncthreads();
-        if (!FWD) {
-            if (t < 64) {
-                double sum = 0.0;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) sum += red[q * 64 + t];
-                rj[t] = rs[J * 64 + t] - sum;
-            }
-            __syncthreads();
-        }
-        {  // x_J[c] = sum_m inv(L_JJ)[c][m] rj[m] (FWD) or inv(L_JJ)[m][c] rj[m] (BWD):
-           // thread (c = t/16, m in 4(t%16)..+3), 16-lane reduction
-            double sum = 0.0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int m = 4 * cg + q;
-                sum += (double)(FWD ? DS[row * TRF_DP + m] : DS[m * TRF_DP + row]) * rj[m];
-            }
-            sum += __shfl_xor(sum, 8, 64);
-            sum += __shfl_xor(sum, 4, 64);
-            sum += __shfl_xor(sum, 2, 64);
-            sum += __shfl_xor(sum, 1, 64);
-            if (cg == 0) {
-                xs[J * 64 + row] = sum;
-                out[b * vstride + J * 64 + row] = sum;
-            }
-        }
-        dv = dnext;
-        __syncthreads();
-    }
-}
+#define TRF_MAXNP 8192  // the multi-workgroup TRSV keeps the solution in LDS (fp64)
 
 // ------------------------------------------------------- multi-workgroup TRSV (G workgroups/chain)
 // The solve of one chain split over G workgroups of 256 threads: workgroup g owns the block steps
@@ -1616,11 +1416,7 @@ void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstri
         attr = true;
     }
     const int np = nb * 64;
-    static int G = 0;
-    if (!G) {  // workgroups per chain (APM_TRSV_G, development knob)
-        const char* e = getenv("APM_TRSV_G");
-        G = e ? std::max(1, std::min(16, atoi(e))) : TRM_G;
-    }
+    const int G = TRM_G;
     hipLaunchKernelGGL(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,
                        np, live);
     if (fwd)
@@ -1629,33 +1425,6 @@ void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstri
     else
         hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * G), dim3(256), lds, s, A, nb,
                            Dinv, dstride, r, out, vstride, live, fail_code, G);
-}
-
-static size_t trf_lds_bytes(int nb) {
-    return sizeof(double) * (2 * nb * 64 + 16 * 64 + 64) + sizeof(float) * 64 * TRF_DP;
-}
-
-bool trsv32_fused_ok(int np) { return np <= TRF_MAXNP; }
-
-void launch_trsv32_fused(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
-                         const double* r, double* out, int64_t vstride, Live live, int nchains,
-                         hipStream_t s) {
-    const size_t lds = trf_lds_bytes(nb);
-    static bool attr = false;
-    if (!attr) {  // dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP)
-        const int mx = (int)trf_lds_bytes(TRF_MAXNP / 64);
-        (void)hipFuncSetAttribute((const void*)k_trsv32_fused<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        (void)hipFuncSetAttribute((const void*)k_trsv32_fused<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        attr = true;
-    }
-    if (fwd)
-        hipLaunchKernelGGL(k_trsv32_fused<true>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
-                           dstride, r, out, vstride, live);
-    else
-        hipLaunchKernelGGL(k_trsv32_fused<false>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
-                           dstride, r, out, vstride, live);
 }
 
 void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,

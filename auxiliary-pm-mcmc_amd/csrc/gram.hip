@@ -139,222 +139,10 @@ __global__ __launch_bounds__(256, 2) void k_gram(MatB K, const double* __restric
     }
 }
 
-// The same super-tiles with the distances in GEMM form on the f64 MFMA (verdict r02 item 6):
-//   s_ij = n_i + n_j - 2 z_i.z_j,  z = x / tau (pre-scaled as above),  n_i = sum_k z_ik^2,
-// z_i.z_j accumulated by v_mfma_f64_16x16x4_f64 (per wave 4x4 blocks of 16x16, A = the i rows and
-// B = the j rows straight from the k-major LDS chunks), the norms in LDS in the k order of the
-// direct form. The subtraction loses ~eps (n_i + n_j) where s_ij << n_i + n_j, so every pair with
-// s_ij < (n_i + n_j) / 2 (cosine of z_i, z_j above 1/2 for equal norms; ~0.1 % of the pairs of the
-// bench's N = 4096, D = 32 data, more for low-dimensional data) is recomputed in the direct form
-// with the direct kernel's arithmetic (same pre-scaling, same fma order); elsewhere the GEMM form's
-// error is at most ~2 ulp of s (tests/test_gpu_kernels.py::_assert_gram_close, 2e-15 relative to
-// the exponent). The MFMAs (D/4 per 16x16 block) leave the VALU to the exp and the fix-ups.
-#define GQ (128 + 2)  // LDS pitch in doubles of the k-major chunks (row r, feature k at [k][r])
-#define ITMAX 256     // features whose 1/tau_k stay in LDS for the fix-ups (beyond: recomputed)
-__global__ __launch_bounds__(256, 2) void k_gram_mfma(MatB K, const double* __restrict__ X,
-                                                      int64_t ldx, int n, int d,
-                                                      const double* __restrict__ theta,
-                                                      int64_t tstride, int kind, double eps,
-                                                      Live live, int both, MatB K2, int k2cols,
-                                                      int nb) {
-    const int b = blockIdx.y;
-    if (live.active[b] == 0 || live.status[b] != 0) return;
-    const int t = blockIdx.x;
-    int si = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (si * (si + 1) / 2 > t) --si;
-    while ((si + 1) * (si + 2) / 2 <= t) ++si;
-    const int sj = t - si * (si + 1) / 2;
-
-    __shared__ __attribute__((aligned(16))) double zi[GK][GQ];
-    __shared__ __attribute__((aligned(16))) double zj[GK][GQ];
-    __shared__ double nrm[2][128];
-    __shared__ double itau[ITMAX];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int r16 = lane & 15, kq = lane >> 4;
-    const int ti = 2 * si + (wv >> 1), tj = 2 * sj + (wv & 1);
-    const bool mine = ti < nb && tj <= ti;
-    const int ro = 64 * (wv >> 1), co = 64 * (wv & 1);
-    const double* th = theta + b * tstride;
-    const double sigma = exp(th[0]);
-    auto itau_of = [&](int k) { return exp(-th[kind == 0 ? 1 : 1 + k]); };
-    for (int k = tid; k < min(d, ITMAX); k += 256) itau[k] = itau_of(k);
-    if (tid < 128) nrm[0][tid] = 0.0;
-    else nrm[1][tid - 128] = 0.0;
-
-    d4_t acc[4][4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = d4_t{0.0, 0.0, 0.0, 0.0};
-
-    for (int k0 = 0; k0 < d; k0 += GK) {
-        const int kc = min(GK, d - k0);
-        __syncthreads();
-        for (int e = tid; e < 128 * GK; e += 256) {
-            const int r = e / GK, k = e % GK;
-            const int gi = si * 128 + r, gj = sj * 128 + r;
-            const double sc = (k < kc) ? (k0 + k < ITMAX ? itau[k0 + k] : itau_of(k0 + k)) : 0.0;
-            zi[k][r] = (k < kc && gi < n) ? X[(int64_t)gi * ldx + k0 + k] * sc : 0.0;
-            zj[k][r] = (k < kc && gj < n) ? X[(int64_t)gj * ldx + k0 + k] * sc : 0.0;
-        }
-        __syncthreads();
-        {  // the 256 rows' norms, features in order (thread = row of zi / zj)
-            const double (*z)[GQ] = tid < 128 ? zi : zj;
-            const int r = tid & 127;
-            double s = nrm[tid >> 7][r];
-            for (int k = 0; k < kc; ++k) s = fma(z[k][r], z[k][r], s);
-            nrm[tid >> 7][r] = s;
-        }
-        if (mine) {
-            for (int k4 = 0; k4 < kc; k4 += 4) {
-                double a[4], c[4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    a[p] = zi[k4 + kq][ro + 16 * p + r16];
-                    c[p] = zj[k4 + kq][co + 16 * p + r16];
-                }
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], c[q], acc[p][q], 0,
-                                                                         0, 0);
-            }
-        }
-    }
-    __syncthreads();  // norms complete
-
-    // f64 MFMA output map: lane l, reg r -> row (l >> 4) + 4r, col l & 15 of block (p, q)
-    if (mine) {
-        // (1) GEMM-form distances; a bit per pair whose subtraction cancels
-        unsigned long long fix = 0;
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int li = ro + 16 * p + kq + 4 * r, lj = co + 16 * q + r16;
-                    const int gi = si * 128 + li, gj = sj * 128 + lj;
-                    const double ni = nrm[0][li], nj = nrm[1][lj];
-                    const double s = ni + nj - 2.0 * acc[p][q][r];
-                    acc[p][q][r] = s;
-                    if (s < 0.5 * (ni + nj) && gi != gj && gi < n && gj < n)
-                        fix |= 1ull << (16 * p + 4 * q + r);
-                }
-        // (2) those pairs in the direct form, one per lane and iteration (rolled: a 64-way
-        // select puts the value in place; the inlined per-pair form overflowed the instruction
-        // cache, a call per pair spilled the accumulators)
-        while (fix) {
-            const int e = __builtin_ctzll(fix);
-            fix &= fix - 1;
-            const int p = e >> 4, q = (e >> 2) & 3, r = e & 3;
-            const int li = ro + 16 * p + kq + 4 * r, lj = co + 16 * q + r16;
-            double sf = 0.0;
-            if (d <= GK) {
-                for (int k = 0; k < d; ++k) {
-                    const double df = zi[k][li] - zj[k][lj];
-                    sf = fma(df, df, sf);
-                }
-            } else {
-                const double* xa = X + (int64_t)(si * 128 + li) * ldx;
-                const double* xc = X + (int64_t)(sj * 128 + lj) * ldx;
-                for (int k = 0; k < d; ++k) {
-                    const double t = k < ITMAX ? itau[k] : itau_of(k);
-                    const double df = xa[k] * t - xc[k] * t;
-                    sf = fma(df, df, sf);
-                }
-            }
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp)
-#pragma unroll
-                for (int qq = 0; qq < 4; ++qq)
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr)
-                        if (16 * pp + 4 * qq + rr == e) acc[pp][qq][rr] = sf;
-        }
-        // (3) K
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = si * 128 + ro + 16 * p + kq + 4 * r;
-                    const int gj = sj * 128 + co + 16 * q + r16;
-                    const double s = acc[p][q][r];
-                    double val;
-                    if (gi < n && gj < n)
-                        val = (gi == gj) ? sigma + eps
-                                         : (GRAM_ABL == 1 ? sigma * s : sigma * exp(-0.5 * s));
-                    else
-                        val = (gi == gj) ? 1.0 : 0.0;
-                    acc[p][q][r] = val;
-                }
-    }
-    if (si == sj) {
-        // Diagonal tiles (waves 0 and 3 of a diagonal super-tile): the entries above the
-        // diagonal take the values of their mirror images below it, so that K is exactly
-        // symmetric as the reference's (kernels.pyx fills K[i,j] and K[j,i] with one value; the
-        // f64 MFMA need not give G_ij and G_ji bit for bit). Through the no longer needed LDS
-        // chunks (wave 0: zi, wave 3: zj, 64 x 65 doubles each), after every wave's fix-ups.
-        __syncthreads();
-        if (mine && ti == tj) {
-            double* Tm = wv == 0 ? &zi[0][0] : &zj[0][0];
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        Tm[(16 * p + kq + 4 * r) * 65 + 16 * q + r16] = acc[p][q][r];
-            // (one wave writes and reads its own region: LDS operations of a wave are ordered)
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-                for (int q = p; q < 4; ++q)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int li = 16 * p + kq + 4 * r, lj = 16 * q + r16;
-                        if (li < lj) acc[p][q][r] = Tm[lj * 65 + li];
-                    }
-        }
-    }
-    if (!mine) return;
-    if (GRAM_ABL == 2 && acc[0][0][0] != -1.0) return;
-    auto store = [&](double* base, int64_t ld) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double* dst = base + (int64_t)(ti * 64 + 16 * p + kq + 4 * r) * ld + tj * 64 + r16;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dst[16 * q] = acc[p][q][r];
-            }
-    };
-    double* Kb = K.base + b * K.cstride;
-    store(Kb, K.ld);
-    if (K2.base && tj < k2cols) store(K2.base + b * K2.cstride, K2.ld);
-    if (both && ti != tj) {  // transposed tile (tj, ti)
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    Kb[(int64_t)(tj * 64 + 16 * q + r16) * K.ld + ti * 64 + 16 * p + kq + 4 * r] =
-                        acc[p][q][r];
-    }
-}
-
 void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const double* theta,
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
-                 hipStream_t s, bool both, MatB K2, int k2cols, bool mfma) {
+                 hipStream_t s, bool both, MatB K2, int k2cols) {
     const int nb = np / 64, ns = (nb + 1) / 2;
-    if (mfma)
-        hipLaunchKernelGGL(k_gram_mfma, dim3(ns * (ns + 1) / 2, nchains), dim3(256), 0, s, K, X,
-                           ldx, n, d, theta, tstride, kind, eps, live, (int)both, K2, k2cols, nb);
-    else
-        hipLaunchKernelGGL(k_gram, dim3(ns * (ns + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx,
-                           n, d, theta, tstride, kind, eps, live, (int)both, K2, k2cols, nb);
+    hipLaunchKernelGGL(k_gram, dim3(ns * (ns + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx, n, d,
+                       theta, tstride, kind, eps, live, (int)both, K2, k2cols, nb);
 }

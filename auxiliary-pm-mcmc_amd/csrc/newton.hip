@@ -262,7 +262,6 @@ void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet
 }
 
 // ------------------------------------------------------------------------------- cache slots
-// mode 0 (IS, augmented): L = C_chol (A rows/cols offset np), row np = g^T (A row 2np, cols >= np)
 // mode 1 (PriorMC):       L = K_chol (A top-left), row np of L = 0
 // mode 2 (IS, chol(K)):   L = (block at rows np.., cols 0..) J, row np = g^T (vector v.Kb)
 // Rows are written whole (upper part zero) because the u-path GEMM streams full row segments.
@@ -276,7 +275,6 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     const int r = blockIdx.x * 4 + w;  // 0 .. np+63
     const double* Ab = A.base + b * A.cstride;
     float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
-    const int64_t off = (mode == 0) ? np : 0;
     double q = 0.0;  // squared norm of factor row r (the wide-slot test, k_slot_write_vec)
     // rows stop at the end of their diagonal tile: k_ugemm reads row r up to column
     // 64 (r / 64 + 1) only (apm_slot_read zeroes the rest on the host)
@@ -289,15 +287,12 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
             q += x * x;
         }
     } else if (r < np) {
-        const double* src = Ab + (off + r) * A.ld + off;
+        const double* src = Ab + (int64_t)r * A.ld;
         for (int c = lane; c < cend; c += 64) {
             const double x = (c <= r) ? src[c] : 0.0;
             L[c] = (float)x;
             q += x * x;
         }
-    } else if (r == np && mode == 0) {
-        const double* src = Ab + (2 * (int64_t)np) * A.ld + np;
-        for (int c = lane; c < np; c += 64) L[c] = (float)src[c];
     } else if (r == np && mode == 2) {
         const double* g = gvec + b * gstride;
         for (int c = lane; c < np; c += 64) L[c] = (float)g[c];
@@ -320,13 +315,12 @@ __global__ __launch_bounds__(256) void k_slot_write_L64(MatB A, SlotSet S,
     const int r = blockIdx.x * 4 + w;  // 0 .. np-1
     const double* Ab = A.base + b * A.cstride;
     double* L = S.L64 + slots[b] * S.l64stride + (int64_t)r * np;
-    const int64_t off = (mode == 0) ? np : 0;
     const int cend = (r / 64 + 1) * 64;  // as k_slot_write_L: k_ugemm64 reads no further
     if (mode == 2) {
         const double* src = Ab + ((int64_t)np + r) * A.ld;
         for (int c = lane; c < cend; c += 64) L[c] = (c <= r) ? src[np - 1 - c] : 0.0;
     } else {
-        const double* src = Ab + (off + r) * A.ld + off;
+        const double* src = Ab + (int64_t)r * A.ld;
         for (int c = lane; c < cend; c += 64) L[c] = (c <= r) ? src[c] : 0.0;
     }
 }

@@ -139,10 +139,9 @@ __device__ __forceinline__ double is_term(double f, double y, double W, double z
     return log_ndtr_mixed(y * f) + (0.5 * W * f - z) * f;
 }
 
-// NSW sample blocks per workgroup (64 x 64 NSW output tile, waves 32 x 32 NSW): NSW = 2 reads L
-// once per two sample blocks (batches of >= UGEMM_W2_MIN chains), NSW = 1 keeps 4x the
-// workgroups for the small batches whose heaviest row block bounds the launch.
-template <int NSW>
+// One 64 x 64 output tile (row block i, sample block sb) per workgroup, waves 32 x 32 (a 64 x 128
+// tile that read L once per two sample blocks was measured slower from 8 chains up: half the
+// workgroups, 2 instead of 4 per CU - DESIGN.md §5).
 __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restrict__ slots,
                                                UPool P, const int64_t* __restrict__ ubufs,
                                                const double* __restrict__ y, int n, int np,
@@ -155,6 +154,7 @@ __global__ __launch_bounds__(256) void k_ugemm(SlotSet S, const int64_t* __restr
     // of U), then sample block fastest - so the nsb
     // workgroups that share row block i's slice of L run together on one XCD and read it once
     // from its L2, and a chain's U stays within one XCD's L2 / the Infinity Cache.
+    constexpr int NSW = 1;
     const int nb = np / 64;
     const int nsg = nsb / NSW;  // sample groups
     const long total = (long)nb * nsg * nchains;
@@ -344,25 +344,13 @@ __global__ __launch_bounds__(256) void k_ugemm64(SlotSet S, const int64_t* __res
     if (tid < 64) pb[(int64_t)i * sp + sb * 64 + tid] = csum[0][tid] + csum[1][tid];
 }
 
-static int UGEMM_W2_MIN = -1;  // batches >= this many chains take k_ugemm<2> (APM_UGEMM_W2_MIN)
-
 void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs,
                   const double* y, int n, int np, double* partial, int64_t pstride,
                   const int* status, int nchains, bool wide, hipStream_t s) {
-    if (UGEMM_W2_MIN < 0) {
-        const char* e = getenv("APM_UGEMM_W2_MIN");
-        UGEMM_W2_MIN = e ? atoi(e) : 1 << 30;
-    }
     const int nb = np / 64, nsb = P.sp / 64;
-    if (nchains >= UGEMM_W2_MIN && nsb % 2 == 0) {
-        const long total = (long)nb * (nsb / 2) * nchains;
-        hipLaunchKernelGGL(k_ugemm<2>, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs,
-                           y, n, np, partial, pstride, status, nsb, nchains);
-    } else {
-        const long total = (long)nb * nsb * nchains;
-        hipLaunchKernelGGL(k_ugemm<1>, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs,
-                           y, n, np, partial, pstride, status, nsb, nchains);
-    }
+    const long total = (long)nb * nsb * nchains;
+    hipLaunchKernelGGL(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
+                       np, partial, pstride, status, nsb, nchains);
     if (wide)
         hipLaunchKernelGGL(k_ugemm64, dim3((unsigned)(nb * nsb), nchains), dim3(256), 0, s, S,
                            slots, P, ubufs, y, n, np, partial, pstride, status, nsb);

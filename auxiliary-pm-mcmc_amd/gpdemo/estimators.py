@@ -61,8 +61,8 @@ class DeviceCache(object):
         """chol(K(theta)) (n, n) lower, computed on the device (fp32-rounded read-back)."""
         if self.kind == _native.EST_PRIORMC:
             return self.read()[0]
-        if self._kchol is not None:
-            return self._kchol
+        if self._kchol is not None:  # a fresh array per call, as the reference's tuple element
+            return self._kchol.copy()
         if self._owner is None or self._theta is None:
             raise ValueError('this cache does not record its theta')
         tmp = self._ctx.slots.acquire()
@@ -71,7 +71,7 @@ class DeviceCache(object):
                                                _UBUF, tmp)
             _raise_for_status(int(st[0]), self._ctx)
             self._kchol = self._ctx.slot_read(tmp)[0]
-            return self._kchol
+            return self._kchol.copy()
         finally:
             self._ctx.slots.release(tmp)
 

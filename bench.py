@@ -703,8 +703,8 @@ def main():
                                               'note': 'direct form sum_k (z_ik - z_jk)^2 on '
                                                       'the fp64 VALU (3 D flops per pair; the '
                                                       'MI355X fp64 vector peak is 78.6 TFLOP/s) '
-                                                      'plus one fp64 exp per pair; the GEMM form '
-                                                      'on the f64 MFMA is APM_GRAM_MFMA=1 '
+                                                      'plus one fp64 exp per pair; a GEMM form '
+                                                      'on the f64 MFMA was measured and declined '
                                                       '(DESIGN.md §5)'}}
     ums, ucnt, uflops = prof['ugemm']
     if ucnt:

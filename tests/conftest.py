@@ -27,9 +27,25 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
 
 
+def _gpu_selected(config):
+    """The run asked for the GPU tests (`-m gpu`, not `-m "not gpu"`)."""
+    expr = (config.getoption('markexpr', '') or '').replace(' ', '')
+    return 'gpu' in expr and 'notgpu' not in expr
+
+
 @pytest.fixture(scope='session')
-def gpu_available():
-    import torch  # only for device discovery on the GPU box
-    if not torch.cuda.is_available():
-        pytest.skip('no GPU')
+def gpu_available(request):
+    """A HIP device seen by libapm.so itself (not torch). A run selected with `-m gpu` on a host
+    where the library or the device is missing FAILS (a broken ROCm runtime must not read as
+    green-with-skips); other selections skip."""
+    from gpdemo import _native
+    try:
+        _native.load_library()
+        ok, why = True, ''
+    except _native.NativeUnavailableError as e:
+        ok, why = False, str(e)
+    if not ok:
+        if _gpu_selected(request.config):
+            pytest.fail('-m gpu run without a usable HIP path: ' + why, pytrace=False)
+        pytest.skip('no GPU: ' + why)
     return True

@@ -76,10 +76,9 @@ def test_gram_large_ragged_vs_c_oracle(nat):
         _assert_gram_close(K, Kr)
 
 
-def test_gram_mfma_fixups_vs_c_oracle(nat, monkeypatch):
-    """k_gram_mfma's direct-form fix-ups (pairs whose GEMM-form distance cancels): near-duplicate
-    rows, D within one LDS chunk (fix-ups from LDS) and beyond it (from global X), iso and ARD;
-    the direct-form kernel (APM_GRAM_MFMA=0) against the same oracle."""
+def test_gram_near_duplicate_rows_vs_c_oracle(nat):
+    """Near-duplicate rows (tiny distances), D within one LDS chunk and beyond it, iso and ARD:
+    the direct-form kernel against the C oracle, and K exactly symmetric."""
     rng = np.random.RandomState(11)
     for n, d, kind in ((200, 3, 'ard'), (150, 40, 'ard'), (130, 6, 'iso')):
         base = rng.normal(size=(n // 2, d))
@@ -88,12 +87,10 @@ def test_gram_mfma_fixups_vs_c_oracle(nat, monkeypatch):
         th = np.r_[0.2, rng.normal(scale=0.5, size=d if kind == 'ard' else 1)]
         Kr = np.empty((n, n))
         orc.c_gram(kind, Kr, X, th, 1e-8)
-        for mfma in ('1', '0'):
-            monkeypatch.setenv('APM_GRAM_MFMA', mfma)
-            K = np.empty((n, n))
-            nat.gram(nat.KERNEL_ISO if kind == 'iso' else nat.KERNEL_ARD, K, X, th, 1e-8)
-            _assert_gram_close(K, Kr)
-            assert np.array_equal(K, K.T)
+        K = np.empty((n, n))
+        nat.gram(nat.KERNEL_ISO if kind == 'iso' else nat.KERNEL_ARD, K, X, th, 1e-8)
+        _assert_gram_close(K, Kr)
+        assert np.array_equal(K, K.T)
 
 
 def test_laplace_vs_golden(nat):
@@ -333,37 +330,6 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
     for b in (0, 1):  # unchanged by the fp32 chain next to them
         np.testing.assert_array_equal(fb1[b], f1[b])
         assert ob1[b] == o1[b]
-
-
-def test_fp16x3_dma_staging_bitwise_equal(nat, monkeypatch):
-    """The LDS-DMA fp16x3 update (APM_H3DMA=1: fp32 operands staged as on the fp32 path, split
-    into hi/lo in registers before the MFMAs) against the register-staged split (default): the same
-    split and the same products in the same order, so the results are bitwise equal - including
-    a theta_0 >= 19 chain on fp32 operands in the same call."""
-    X, y, thetas, ns = _mixed_case()
-    th = thetas.copy()
-    th[2, 0] = 19.5
-    o0, s0, n0, f0 = _run_is(nat, X, y, th, ns, monkeypatch)
-    o1, s1, n1, f1 = _run_is(nat, X, y, th, ns, monkeypatch, APM_H3DMA=1)
-    np.testing.assert_array_equal(s1, s0)
-    np.testing.assert_array_equal(n1, n0)
-    for b in range(len(th)):
-        np.testing.assert_array_equal(f1[b], f0[b])
-        assert o1[b] == o0[b] or (np.isnan(o1[b]) and np.isnan(o0[b])), (b, o1[b], o0[b])
-
-
-def test_multi_workgroup_trsv_matches_single(nat, monkeypatch):
-    """The Newton solves' 4-workgroup TRSV (k_trsv32_mw, default) against the one-workgroup
-    kernel (APM_TRSV_MW=0): modes to 1e-9 relative (summation order only, amplified by the Newton
-    update f = K a; both agree with the all-fp64 path to ~5e-10 at N=700)."""
-    X, y, thetas, ns = _mixed_case()
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_TRSV_MW=0)
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
-    assert (s0 == 0).all() and (s1 == 0).all()
-    np.testing.assert_array_equal(n1, n0)
-    for b in range(len(thetas)):
-        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-9, atol=1e-9 * np.abs(f0[b]).max())
-        assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
 
 
 @pytest.mark.parametrize('n', [560, 1100])

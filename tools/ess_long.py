@@ -1,11 +1,20 @@
 """Long-chain ESS / R-hat record (Analyse results.ipynb:138-141, E-SS+RD-SS.ipynb:64):
 C independent APM E-SS(u) + RD-SS(theta) chains at BASELINE configs[2] (N=4096 D=32 ARD, N_imp=256)
-on one MI355X, 500 warm-up transitions per chain discarded, >= 2000 kept; coda effectiveSize and
-gelman.diag restated (auxpm/diagnostics.py) on the kept draws; wall time of the kept segment.
+on one MI355X, `--warmup` transitions per chain discarded; coda effectiveSize and gelman.diag
+restated (auxpm/diagnostics.py) on the kept draws, with the R-hat trajectory over the run.
 
-    python tools/ess_long.py [--chains 16 --warmup 500 --keep 2000] > out.json
+The run is split into segments of at most `--max-seconds` of sampling (one gpurun call each):
+every segment writes the chains' checkpoint (auxpm.batched ``checkpoint``: host state + the u
+history, no u arrays) and its own theta draws (float32) to `--out-dir`; the next segment is started
+with `--resume-dir` pointing at a directory holding all earlier segments' files, rebuilds u on the
+device, checks that the recomputed current estimates equal the saved ones, and continues the same
+chains. The summary covers every segment so far.
+
+    python tools/ess_long.py --chains 64 --max-seconds 1000 --out-dir gpurun_out/ess_seg0
+    python tools/ess_long.py --chains 64 --resume-dir ess_state --out-dir gpurun_out/ess_seg1
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -17,67 +26,143 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'auxiliary-pm-mcmc_amd'))
 
 
+def load_series(dirs):
+    """All segments' draws, in segment order: (C, T, P) float64."""
+    files = {}
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, 'series_seg*.npy')):
+            files[os.path.basename(f)] = f
+    parts = [np.load(files[k]) for k in sorted(files)]
+    return (np.concatenate(parts, axis=1).astype(np.float64) if parts else None), len(parts)
+
+
+def summarise(series, live, warmup, seg_walls, seg_transitions, cfg):
+    from auxpm.diagnostics import effective_size, gelman_rubin
+    T = series.shape[1]
+    kept = series[live, warmup:T]
+    keep = kept.shape[1]
+    traj = []
+    step = 500
+    for L in list(range(step, keep, step)) + [keep]:
+        r = gelman_rubin(kept[:, :L])
+        traj.append({'kept_per_chain': int(L), 'transitions_per_chain': int(warmup + L),
+                     'rhat_max': float(r.max()), 'rhat_median': float(np.median(r))})
+    ess = np.stack([effective_size(kept[q]) for q in range(kept.shape[0])])  # (C, P)
+    rhat = gelman_rubin(kept)
+    crossed = next((t['transitions_per_chain'] for t in traj if t['rhat_max'] < 1.1), None)
+    wall = float(sum(seg_walls))
+    ntr = int(sum(seg_transitions))
+    tps = ntr / wall if wall > 0 else None
+    ept_min = float(ess.min(1).mean() / keep)
+    ept_mean = float(ess.mean(1).mean() / keep)
+    return {
+        'what': 'long-chain ESS / R-hat at BASELINE configs[2] (SURVEY.md §8d protocol), '
+                'checkpointed segments on one MI355X',
+        'config': cfg,
+        'segments': len(seg_walls),
+        'failed_chains': int(series.shape[0] - len(live)),
+        'transitions_per_chain': int(T), 'warmup_discarded': int(warmup), 'kept_per_chain': int(keep),
+        'sampling_wall_s': wall,
+        'transitions_per_s_sampling': tps,
+        'ess_min_per_chain_mean': float(ess.min(1).mean()),
+        'ess_min_per_chain_median': float(np.median(ess.min(1))),
+        'ess_mean_per_chain_mean': float(ess.mean(1).mean()),
+        'ess_per_transition_min_component': ept_min,
+        'ess_per_transition_mean_component': ept_mean,
+        'ess_per_transition_min_component_worst_chain': float(ess.min(1).min() / keep),
+        'ess_per_sec_min_component': ept_min * tps if tps else None,
+        'ess_per_sec_mean_component': ept_mean * tps if tps else None,
+        'rhat_max': float(rhat.max()), 'rhat_median': float(np.median(rhat)),
+        'rhat_argmax_component': int(rhat.argmax()),
+        'rhat_theta0_log_sigma': float(rhat[0]),
+        'rhat_below_1p1_at_transitions_per_chain': crossed,
+        'rhat_trajectory': traj,
+        'posterior_mean_log_sigma': float(kept[:, :, 0].mean()),
+        'method': 'coda effectiveSize / gelman.diag restatements (auxpm/diagnostics.py) on the '
+                  'kept draws of every live chain; ESS per transition = mean over chains of the '
+                  'min (or mean) over the 33 theta components of ESS / kept length; ESS/s = that '
+                  'x the sampling throughput (all chains, all segments: transitions / wall)',
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--chains', type=int, default=16)
+    ap.add_argument('--chains', type=int, default=64)
     ap.add_argument('--warmup', type=int, default=500)
-    ap.add_argument('--keep', type=int, default=2000)
+    ap.add_argument('--target', type=int, default=9000, help='transitions per chain in total')
     ap.add_argument('--chunk', type=int, default=100)
+    ap.add_argument('--max-seconds', type=float, default=1000.)
+    ap.add_argument('--resume-dir', default=None)
+    ap.add_argument('--out-dir', required=True)
     ap.add_argument('--n', type=int, default=4096)
     ap.add_argument('--d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
     a = ap.parse_args()
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
-    from auxpm.diagnostics import effective_size, gelman_rubin
     from gpdemo.utils import synthetic_gp_data
+    os.makedirs(a.out_dir, exist_ok=True)
+    t_start = time.perf_counter()
     X, y = synthetic_gp_data(a.n, a.d, a.seed)
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    cfg = {'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'chains': a.chains,
+           'seed': a.seed, 'kernel': 'ard', 'epsilon': 1e-8, 'w': 1., 'max_steps_out': 0}
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
         seed=a.seed + 1)
-    smp.initialise()
-    series = [[] for _ in range(a.chains)]
-    t_start = time.perf_counter()
-    t_keep = None
-    total = a.warmup + a.keep
-    have = 0
-    while have < total:
-        if have == a.warmup:
-            t_keep = time.perf_counter()
-        step = min(a.chunk, (a.warmup if have < a.warmup else total) - have)
+    dirs = [a.resume_dir] if a.resume_dir else []
+    prev, n_seg = load_series(dirs)
+    have = 0 if prev is None else prev.shape[1]
+    meta = {'seg_walls': [], 'seg_transitions': []}
+    restore_dlogf = None
+    if a.resume_dir:
+        with np.load(os.path.join(a.resume_dir, 'state.npz')) as z:
+            ck = {k: z[k] for k in z.files}
+        with open(os.path.join(a.resume_dir, 'meta.json')) as f:
+            meta = json.load(f)
+        if int(ck['transitions_per_chain']) != have:
+            raise RuntimeError('checkpoint at {0} transitions, series hold {1}'.format(
+                int(ck['transitions_per_chain']), have))
+        restore_dlogf = smp.restore(ck)
+        print('resumed at {0} transitions per chain; max |d log f| on restore {1:.3g} ({2:.0f} s)'
+              .format(have, restore_dlogf, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+        if not restore_dlogf <= 1e-9:
+            raise RuntimeError('restored chains differ from the checkpoint: {0}'.format(restore_dlogf))
+    else:
+        smp.initialise()
+    seg = [[] for _ in range(a.chains)]
+    t0 = time.perf_counter()
+    done_here = 0
+    while have + done_here < a.target and time.perf_counter() - t0 < a.max_seconds:
+        step = min(a.chunk, a.target - have - done_here)
         tr, done = smp.run_async(step)
         for c in range(a.chains):
-            series[c].extend(tr[c])
-        have += step
-        print('{0} / {1} transitions per chain, {2:.0f} s'.format(
-            have, total, time.perf_counter() - t_start), file=sys.stderr, flush=True)
-    wall_keep = time.perf_counter() - t_keep
+            if smp.failed[c]:
+                tr[c] = tr[c] + [smp.theta[c].copy()] * (step - len(tr[c]))
+            seg[c].extend(tr[c])
+        done_here += step
+        print('{0} / {1} transitions per chain, segment {2:.0f} s'.format(
+            have + done_here, a.target, time.perf_counter() - t0), file=sys.stderr, flush=True)
+    wall = time.perf_counter() - t0
     live = [c for c in range(a.chains) if not smp.failed[c]]
-    kept = np.stack([np.array(series[c][a.warmup:total]) for c in live])   # (C, keep, P)
-    ess = np.stack([effective_size(kept[q]) for q in range(len(live))])     # (C, P)
-    rhat = gelman_rubin(kept)
-    out = {
-        'what': 'long-chain ESS / R-hat at BASELINE configs[2] (SURVEY.md §8d protocol)',
-        'config': {'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'chains': a.chains,
-                   'warmup_discarded': a.warmup, 'kept_per_chain': a.keep, 'seed': a.seed},
-        'failed_chains': int(smp.failed.sum()),
-        'wall_s_kept_segment': wall_keep,
-        'transitions_per_s_kept_segment': len(live) * a.keep / wall_keep,
-        'ess_min_per_chain_mean': float(ess.min(1).mean()),
-        'ess_min_per_chain_median': float(np.median(ess.min(1))),
-        'ess_mean_per_chain_mean': float(ess.mean(1).mean()),
-        'ess_per_transition_min_component': float(ess.min(1).mean() / a.keep),
-        'ess_per_sec_min_component': float(ess.min(1).sum() / wall_keep),
-        'ess_per_sec_mean_component': float(ess.mean(1).sum() / wall_keep),
-        'rhat_max': float(rhat.max()), 'rhat_median': float(np.median(rhat)),
-        'rhat_theta0_log_sigma': float(rhat[0]),
-        'posterior_mean_log_sigma': float(kept[:, :, 0].mean()),
-        'method': 'coda effectiveSize / gelman.diag restatements (auxpm/diagnostics.py); ESS per '
-                  'chain = min (or mean) over the theta components; ESS/s = sum over chains / '
-                  'wall time of the kept segment',
-    }
-    print(json.dumps(out), flush=True)
+    meta['seg_walls'].append(wall)
+    meta['seg_transitions'].append(int(done_here * len(live)))
+    meta.setdefault('restore_dlogf', []).append(restore_dlogf)
+    np.save(os.path.join(a.out_dir, 'series_seg{0:02d}.npy'.format(n_seg)),
+            np.array(seg, dtype=np.float32))
+    ck = smp.checkpoint()
+    ck['transitions_per_chain'] = np.int64(have + done_here)
+    np.savez(os.path.join(a.out_dir, 'state.npz'), **ck)
+    with open(os.path.join(a.out_dir, 'meta.json'), 'w') as f:
+        json.dump(meta, f)
+    series, _ = load_series(dirs + [a.out_dir])
+    out = summarise(series, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
+    out['restore_max_abs_dlogf'] = meta['restore_dlogf']
+    with open(os.path.join(a.out_dir, 'summary.json'), 'w') as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in ('transitions_per_chain', 'rhat_max', 'rhat_median',
+                                          'ess_per_transition_min_component',
+                                          'transitions_per_s_sampling')}), flush=True)
 
 
 if __name__ == '__main__':
