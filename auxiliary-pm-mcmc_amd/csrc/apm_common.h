@@ -13,6 +13,7 @@
 
 typedef double d4_t __attribute__((ext_vector_type(4)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
 typedef double d2_t __attribute__((ext_vector_type(2)));
 
 // per-chain status codes (mirrored in gpdemo/_native.py)

@@ -84,6 +84,18 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base,
                             unsigned long long* timeouts, hipStream_t s);
+// rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is final (fd.Dinv: its
+// inverses), each row a left-looking walk over the panel's columns with no waits; zrow > 0: row
+// tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)
+void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
+                              FusedDiag<float> fd, Live live, int nchains, int hlim,
+                              const int* h3ok, hipStream_t s);
+// the same rows solved right-looking with each row's panel tiles in registers (chol32.hip
+// k_panel_rows32): ncols <= RP_NCOLS; Dinv / dstride: the diagonal tiles' fp32 inverses
+#define RP_NCOLS 8
+void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, const float* Dinv,
+                         int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
+                         hipStream_t s);
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
@@ -184,16 +196,24 @@ struct SlotSet {
     int* chain_wide;    // 1 per chain of the call (read back with the theta-call's results)
     int64_t l64stride;
     double wide_q;      // the threshold (APM_WIDE_Q, overridable by the environment variable)
+    double post_q;      // trace(C) above which an fp32 bottom block is recomputed in fp64
+                        // (APM_POST32_Q; postcov.hip)
 };
 // trace(L L^T) above which a slot's u-path runs in fp64: the fp32 L.U moves
 // log f by ~1e-10 x trace (11 nats at trace 1.15e11, sigma = e^18.5; < 1e-6 nats at the trace
 // ~1e3 of typical thetas), so this keeps the fp32 rounding of L and U below ~1e-4 nats
 #define APM_WIDE_Q 1.0e6
+// trace(C) above which the posterior factor's bottom block is recomputed in fp64 (postcov.hip):
+// its fp32 TRSM moves log f by ~1e-9 x trace(C) (tools/postcov_precision_study.py)
+#define APM_POST32_Q 1.0e5
 // write slot slots[b] from the factored work matrix. mode 1 = PriorMC (K_chol at (0,0), g = 0),
-// mode 2 = IS via chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb)
+// mode 2 = IS via chol(K) (postcov.hip: chol(C) J at rows [np, 2np) cols [0, np), g in v.Kb),
+// mode 3 = the same with chol(C) J in the fp32 bottom block of S32 (rows [np, 2np)); its chains
+// with trace(C) > S.post_q get bit 1 of S.chain_wide (the host recomputes them in fp64, mode 2).
+// Only chains with live.active[b] && !live.status[b] are written.
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
-                       int nchains, hipStream_t s);
+                       int nchains, hipStream_t s, MatF S32 = MatF{nullptr, 0, 0});
 
 // ---- postcov.hip ----------------------------------------------------------------------------
 void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,
@@ -209,6 +229,14 @@ void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s
 // out = L^T x (L lower), or with rev g = J L^T J h; tile-parallel through nb*nb*64 partials per chain
 void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t vstride, int np,
                        double* part, int64_t pstride, Live live, int nchains, hipStream_t s);
+// fp32 working copy of the posterior factor for its bottom block (postcov.hip): S32's top rows
+// <- the lower tiles of the fp64 top factor L' (rows [0, np) of A) in tile columns [k0, k1), its
+// diagonal-tile inverses D32 <- D64 for those columns; bottom: S32's rows [np, 2np) <- L_K J
+// (rows [np, 2np) of A) from the outer panel of each row's first nonzero tile on (the zero
+// tiles the bottom's updates read included)
+void launch_post32_convert(MatB A, MatF S32, const double* D64, int64_t d64stride, float* D32,
+                           int64_t d32stride, int nb, int outer, int k0, int k1, bool bottom,
+                           Live live, int nchains, hipStream_t s);
 // status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)
 void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s);
 

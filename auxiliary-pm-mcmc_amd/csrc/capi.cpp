@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -90,11 +91,20 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
-    bool h3 = true;       // APM_H3=0: fp32 operands in the Newton factor's outer updates
+    bool h3 = true;       // APM_H3=0: fp32 operands in the fp32 factorisations' outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
-    // dataflow in-panel factorisation of the Newton matrix (APM_DF32=0: the launch sequence)
-    bool df32 = true;
+    int* h3post = nullptr;  // the same for the posterior factor's fp32 bottom block (h3ok + B)
+    // the bottom block of the posterior factor [[J M J],[L_K J]] (the TRSM that yields chol(C) J)
+    // in fp32 after the fp64 factorisation of J M J (postcov.hip; APM_POST32=0: all fp64); chains
+    // whose trace(C) exceeds Sl.post_q are recomputed in fp64 (n_post64 counts them)
+    int post32 = 2;  // 1: after the fp64 factorisation of J M J; 2: panel by panel beside it
+    int* hmask = nullptr;  // pinned: the chains of such a recomputation
+    int64_t n_post64 = 0;
+    // in-panel factorisation of the Newton matrix: 2 (default) the diagonal block's dataflow chain
+    // then the rows below it by the row-panel TRSM (k_panel_rows32); 1 every row by the dataflow
+    // walk (k_chol_panel_df32); 0 the launch sequence both replace (APM_DF32)
+    int df32 = 2;
     unsigned long long* dfprog = nullptr;  // per (chain, row tile) progress words
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
@@ -284,9 +294,12 @@ void tracked_update(apm_ctx* c, MatB M, int k0, int kc, int i0, int R, int j0, i
 // diag: its one-wave latency hides under that launch instead of idling the GPU between launches).
 // row_start > 0 restricts every panel solve and update to rows >= row_start (the top-left of the
 // augmented matrix is already factored); factor_diag = false reuses L_kk and inv(L_kk).
+// after_panel(K, Kend): called (host side) once the panel's columns are final, before its outer
+// update is enqueued (the posterior factor's fp32 bottom block follows the panels on stream2).
 void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code, int count,
                 bool factor_diag = true, int row_start = 0, GapFn gap = no_gap,
-                const Exec* ex = nullptr, const MatB* first_src = nullptr) {
+                const Exec* ex = nullptr, const MatB* first_src = nullptr,
+                const std::function<void(int, int)>& after_panel = nullptr) {
     const Exec E = ex ? *ex : main_exec(c);
     const Live lv = E.lv;
     const bool fuse = factor_diag && row_start <= k0;
@@ -310,6 +323,7 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
                                   E.s);
                 check_launch();
             }
+            if (after_panel) after_panel(K, Kend);
             have_diag = Kend < k1;
             tracked_update(c, M, K, Kend - K, Kend, R, Kend, Cb, gap(Kend - 1, c->nb), false,
                            count, have_diag ? Kend : -1, fail_code, &E, K == k0 ? first_src : nullptr);
@@ -397,7 +411,8 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
-            if (!launch_chol_panel_df32(M, K, Kend - K, R,
+            const bool rp = c->df32 == 2 && Kend - K <= RP_NCOLS;
+            if (!launch_chol_panel_df32(M, K, Kend - K, rp ? std::min(R, Kend) : R,
                                         FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code},
                                         lv, count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog,
                                         c->nb + 1,
@@ -405,6 +420,11 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                         c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream))
                 throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
+            if (rp) {  // the rows below the diagonal block, once it is factored
+                launch_panel_rows32(M, K, Kend - K, Kend, R, 0, D, ds, lv, count,
+                                    c->h3_now ? c->nb : 0, c->h3ok, c->stream);
+                check_launch();
+            }
             have_diag = Kend < k1;
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                              fail_code);
@@ -472,6 +492,7 @@ void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubuf
                             c->stream));
 }
 int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 16 * c->max_batch); }
+int* pin_h3post(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 20 * c->max_batch); }
 
 // per-chain fp16x3 flags of a theta-call -> device (chol32.hip: |L_ij| <= sqrt(1 + K_ii) must
 // stay below fp16's range); h3_now = any chain flagged (else the fp32-operand kernel launches)
@@ -480,6 +501,8 @@ void upload_h3(apm_ctx* c, int count) {
     c->h3_now = false;
     for (int b = 0; b < count; ++b) c->h3_now |= h[b] != 0;
     HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->h3post, pin_h3post(c), sizeof(int) * count, hipMemcpyHostToDevice,
+                        c->stream));
 }
 
 // wide: some slot of the call may be wide (theta-calls: unknown until the read-back; u-calls:
@@ -742,6 +765,100 @@ Exec k_exec(apm_ctx* c, hipStream_t s) {
                 c->cholk_count};
 }
 
+// The bottom block of [[J M J],[L_K J]] after the fp64 factorisation of J M J = L' L'^T: the TRSM
+// (L_K J) L'^-T = chol(C) J as a blocked right-looking solve in fp32 on a working copy S32 in
+// the free right half of A (postcov.hip): per outer panel of L', the rows' left-looking walks over
+// the panel's columns (the dataflow kernel's no-wait twin, k_chol_panel_df32<true>, against the
+// fp32 inverses of L''s diagonal tiles), then the rank-64*outer update of the rows' remaining
+// columns on the 128x128 super-tile kernel (fp16x3 operands where h3post allows). Row tile nb + I
+// of L_K J is zero before tile column nb - 1 - I (chol(C) J keeps that pattern), so a panel
+// touches only the rows whose first nonzero tile lies in or before it. The fp64 route costs N^3/3
+// flops per chain on the f64 MFMA; chol(C) enters the estimate only through the fp32 slot and
+// L.U, and moves log f by ~1e-9 x trace(C) in fp32 (tools/postcov_precision_study.py), so chains
+// with trace(C) > Sl.post_q are recomputed in fp64 after the slot write (bottom64_rerun).
+MatF s32_of(apm_ctx* c) {
+    return MatF{reinterpret_cast<float*>(c->A.base + c->np), 2 * c->A.ld, 2 * c->A.cstride};
+}
+float* d32post_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv + (int64_t)c->nb * 4096); }
+
+// one outer panel [K, Kend) of the bottom block on stream s: the rows' walks, then the update of
+// their remaining columns
+void post_bottom32_steps(apm_ctx* c, int count, int K, int Kend, hipStream_t s) {
+    const Live lv = live_of(c);
+    const int nb = c->nb;
+    MatF S = s32_of(c);
+    const int64_t ds32 = 2 * c->dstride;
+    const int hlim = c->h3 ? 2 * nb : 0;
+    const int row0 = std::max(nb, 2 * nb - Kend);  // rows with a nonzero tile in the panel
+    if (c->df32 == 2 && Kend - K <= RP_NCOLS)
+        launch_panel_rows32(S, K, Kend - K, row0, 2 * nb, 2 * nb, d32post_of(c), ds32, lv, count,
+                            hlim, c->h3post, s);
+    else
+        launch_chol_panel_bulk32(S, K, Kend - K, row0, 2 * nb, 2 * nb,
+                                 FusedDiag<float>{0, d32post_of(c), ds32, nullptr, 0, 0}, lv,
+                                 count, hlim, c->h3post, s);
+    check_launch();
+    if (Kend >= nb) return;
+    const auto sl = super_list(c, row0, 2 * nb, Kend, nb, Gap{0, 0});
+    const double fl =
+        c->prof ? update_flops(row0, 2 * nb, Kend, nb, Kend - K, Gap{0, 0}) * c->live_n : 0.0;
+    ProfScope ps(c, APM_PROF_POST32_OUTER, fl, s);
+    launch_chol_update32_t128(S, K, Kend - K, sl.first, sl.second, lv, count, s,
+                              FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, hlim, c->h3post);
+    check_launch();
+}
+
+// APM_POST32=1: the whole bottom block after the fp64 factorisation of J M J, on the main stream
+void post_bottom32(apm_ctx* c, int count) {
+    const int nb = c->nb;
+    launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride, nb,
+                          c->outer, 0, nb, true, live_of(c), count, c->stream);
+    check_launch();
+    for (int K = 0; K < nb; K += c->outer)
+        post_bottom32_steps(c, count, K, std::min(K + c->outer, nb), c->stream);
+}
+
+// APM_POST32=2 (default): the bottom block's copy once L_K J is formed, then each outer panel of
+// the bottom on the low-priority stream2 as soon as the fp64 factorisation has finished that
+// panel of L' (post_bottom32_panel, chol_range's after_panel): the bottom's fp32 work fills the
+// CUs the fp64 in-panel steps leave idle instead of following the factorisation
+void post_bottom32_begin(apm_ctx* c, int count) {
+    HIPC(hipEventRecord(c->ev_gram, c->stream));
+    HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
+    launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride,
+                          c->nb, c->outer, 0, 0, true, live_of(c), count, c->stream2);
+    check_launch();
+}
+void post_bottom32_panel(apm_ctx* c, int count, int K, int Kend) {
+    hipEvent_t e = c->ev_feed[c->feed_i++ & 3];
+    HIPC(hipEventRecord(e, c->stream));
+    HIPC(hipStreamWaitEvent(c->stream2, e, 0));
+    launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride,
+                          c->nb, c->outer, K, Kend, false, live_of(c), count, c->stream2);
+    check_launch();
+    post_bottom32_steps(c, count, K, Kend, c->stream2);
+}
+
+// The fp64 bottom block for the chains flagged by the slot writer (bit 1 of Sl.chain_wide):
+// (L_K J) L'^-T on the still intact fp64 rows [np, 2np) of A and L' (chol_range restricted to
+// those rows, the chains masked through active2), then their slots again in mode 2 and the u-path
+// of the call again (the other chains' values are recomputed unchanged).
+void bottom64_rerun(apm_ctx* c, int count, const std::vector<int>& redo) {
+    const int nb = c->nb;
+    for (int b = 0; b < count; ++b) c->hmask[b] = 0;
+    for (int b : redo) c->hmask[b] = 1;
+    HIPC(hipMemcpyAsync(c->active2, c->hmask, sizeof(int) * count, hipMemcpyHostToDevice,
+                        c->stream));
+    const Live lr{c->active2, c->status};
+    const Exec ex{c->stream, lr, c->Dinv, c->ldet, (int)redo.size()};
+    chol_range(c, c->A, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, /*factor_diag=*/false,
+               /*row_start=*/nb, y_gap, &ex);
+    launch_slot_write(c->A, c->v, c->ldet, c->lstride, nb, c->Sl, c->d_slots, 2, c->n, c->np, lr,
+                      count, c->stream);
+    check_launch();
+    c->n_post64 += (int64_t)redo.size();
+}
+
 // L_K ready in BL (chol_k_into_bl); h = L_K^-1 f_post = L_K^T a because f_post = K a
 void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     const Live lv = live_of(c);
@@ -780,10 +897,24 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
             tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, 1, count);
         }
     }
-    chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
+    if (!c->post32) {
+        chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
+    } else if (c->post32 == 1) {  // J M J alone in fp64 (its log-determinant is log|B|)
+        chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count);
+    } else {  // ... with the fp32 bottom block following its panels on stream2
+        post_bottom32_begin(c, count);
+        chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count, true, 0, no_gap, nullptr,
+                   nullptr, [c, count](int K, int Kend) { post_bottom32_panel(c, count, K, Kend); });
+    }
     launch_trmv_tiles(true, TL, c->v.z, c->v.Kb, vs, np, c->sympart, c->sstride, lv, count,
                       s);                                                     // g = J L'^T J h
     check_launch();
+    if (c->post32 == 1) {
+        post_bottom32(c, count);
+    } else if (c->post32 == 2) {  // the slot writer reads the bottom block: join stream2
+        HIPC(hipEventRecord(c->ev_cholk, c->stream2));
+        HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
+    }
 }
 
 void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf, int* status,
@@ -858,8 +989,8 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             check_launch();
         } else {
             post_cov_lk(c, count, ov);
-            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots, 2,
-                              c->n, c->np, lv, count, c->stream);
+            launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots,
+                              c->post32 ? 3 : 2, c->n, c->np, lv, count, c->stream, s32_of(c));
             check_launch();
             u_eval_device(c, count, true);
         }
@@ -874,9 +1005,19 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                       RB{c->status, (int)sizeof(int) * count, st_h.data()},
                       RB{c->n_iter, (int)sizeof(int) * count, it_h.data()},
                       RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
+        std::vector<int> redo;  // fp32 bottom blocks above the trace bound (slot bit 1)
+        for (int b = 0; b < count; ++b)
+            if (st_h[b] == 0 && (wide_h[b] & 2)) redo.push_back(b);
+        if (!redo.empty() && est == APM_EST_IS) {
+            bottom64_rerun(c, count, redo);
+            u_eval_device(c, count, true);
+            read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
+                          RB{c->status, (int)sizeof(int) * count, st_h.data()},
+                          RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
+        }
         const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
         for (int b = 0; b < count; ++b)
-            if (st_h[b] == 0) c->slot_wide[hs[b]] = wide_h[b];
+            if (st_h[b] == 0) c->slot_wide[hs[b]] = wide_h[b] & 1;
     }
     for (int b = 0; b < count; ++b) {
         status[b] = st_h[b];
@@ -906,11 +1047,11 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_OUTER32")) c->outer32 = std::min(14, std::max(1, atoi(e)));
     HIPC(hipSetDevice(device));
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
-    if (const char* e = getenv("APM_REFINE")) c->n_refine = std::max(0, atoi(e));
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
-    if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
+    if (const char* e = getenv("APM_DF32")) c->df32 = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -975,11 +1116,14 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 20, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 24, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hmask), sizeof(int) * (size_t)B,
+                       hipHostMallocDefault));
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 20,
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
-    c->h3ok = dalloc<int>(c, B);
+    c->h3ok = dalloc<int>(c, 2 * B);
+    c->h3post = c->h3ok + B;
     // + 1: the count of bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS)
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 1);
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 1)));
@@ -999,8 +1143,11 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
                     dalloc<double>(c, n_slots * np), dalloc<double>(c, n_slots * np),
                     dalloc<double>(c, n_slots), Lsz, np,
                     dalloc<double>(c, n_slots * np * np), dalloc<double>(c, n_slots * np),
-                    dalloc<int>(c, n_slots), dalloc<int>(c, B), np * np, APM_WIDE_Q};
+                    dalloc<int>(c, n_slots), dalloc<int>(c, B), np * np, APM_WIDE_Q,
+                    APM_POST32_Q};
     if (const char* e = getenv("APM_WIDE_Q")) c->Sl.wide_q = atof(e);  // development knob
+    if (const char* e = getenv("APM_POST32_Q")) c->Sl.post_q = atof(e);
+    c->Sl.post_q = std::min(c->Sl.post_q, c->Sl.wide_q);  // (a wide slot needs the fp64 factor)
     HIPC(hipMemset(c->Sl.cst, 0, sizeof(double) * n_slots));
     HIPC(hipMemset(c->Sl.wide, 0, sizeof(int) * n_slots));
     c->slot_wide.assign((size_t)n_slots, 0);
@@ -1019,6 +1166,7 @@ void free_ctx(apm_ctx* c) {
     if (c->hblk) (void)hipHostFree(c->hblk);
     if (c->hth) (void)hipHostFree(c->hth);
     if (c->hx) (void)hipHostFree(c->hx);
+    if (c->hmask) (void)hipHostFree(c->hmask);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1189,8 +1337,12 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
             for (int p = 0; p < c->P; ++p) th[b * c->P + p] = thetas[b * ldt + p];
         HIPC(hipMemcpyAsync(c->theta, th, sizeof(double) * count * c->P, hipMemcpyHostToDevice,
                             c->stream));
-        // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip): per chain
-        for (int64_t b = 0; b < count; ++b) pin_h3(c)[b] = c->h3 && th[b * c->P] < 19.0;
+        // fp16x3 Newton updates need |L_ij| <= sqrt(1 + K_ii) < 65504 (chol32.hip): per chain;
+        // the posterior bottom block's operands |L'_ij| <= sqrt(1 + n K_ii) (postcov.hip)
+        for (int64_t b = 0; b < count; ++b) {
+            pin_h3(c)[b] = c->h3 && th[b * c->P] < 19.0;
+            pin_h3post(c)[b] = c->h3 && 1.0 + c->n * (std::exp(th[b * c->P]) + c->eps) < 4e8;
+        }
         upload_h3(c, (int)count);
         if (est != APM_EST_LAPLACE) upload_idx(c, (int)count, slots, ubufs);
         theta_eval_impl(c, est, (int)count, true, out_logf, status, nops);
@@ -1221,6 +1373,7 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
         double kmax = 0.0;
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
         pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
+        pin_h3post(c)[0] = c->h3 && 1.0 + c->n * kmax < 4e8;
         upload_h3(c, 1);
         upload_idx(c, 1, &slot, &ubuf);  // (the pinned copy is the slot the read-back marks)
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);
@@ -1506,6 +1659,13 @@ int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, dou
             if (launches) *launches = (int64_t)h;
             if (work) *work = 0.0;
             if (reset) HIPC(hipMemset(d, 0, sizeof(h)));
+            return APM_SUCCESS;
+        }
+        if (kind == APM_PROF_POST64_RERUNS) {
+            if (total_ms) *total_ms = 0.0;
+            if (launches) *launches = c->n_post64;
+            if (work) *work = 0.0;
+            if (reset) c->n_post64 = 0;
             return APM_SUCCESS;
         }
         if (kind == APM_PROF_STATS) {

@@ -372,12 +372,12 @@ __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float*
 #ifndef DF_BULK_WPE
 #define DF_BULK_WPE 3  // ... and of its bulk-row twin (no diagonal factorisation, no waits)
 #endif
-// BULK = false: rows [K, Kend + ...) as described above (with the split launch: rows [K, Kend)
-// only, the diagonal block). BULK = true: the rows below the diagonal block, [Kend, R), after
-// the diagonal block's launch: the same row walk (same operands, same accumulation order: bitwise
-// the same tiles) without the waits - every diagonal tile is final - and without the diagonal
-// factorisation code, whose registers held the combined kernel at 2 workgroups per CU while the
-// bulk rows' walks (~13 us per column, latency-bound) are throughput-limited by residency.
+// BULK = false: rows [K, R) as described above. BULK = true: rows [row0, R) below an outer panel
+// whose diagonal block is already factored (every diagonal tile and its inverse final): the same
+// row walk without the waits and without the diagonal factorisation code (whose registers hold
+// the combined kernel at 2 workgroups per CU). Used for the fp32 bottom block of the posterior
+// factor (postcov.hip): with zrow > 0, row tile i is zero in the tile columns < zrow - 1 - i (the
+// anti-triangular L_K J), so its walk starts at column max(K, zrow - 1 - i) and reads no zero tile.
 template <bool BULK>
 __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel_df32(MatF A, int K, int ncols, int R, int nchains,
                                                          FusedDiag<float> fd, Live live, int hlim,
@@ -385,7 +385,8 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          unsigned long long* prog,
                                                          int64_t pstride,
                                                          unsigned long long base,
-                                                         unsigned long long* timeouts) {
+                                                         unsigned long long* timeouts,
+                                                         int row0 = 0, int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -399,11 +400,11 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
         // runs on XCD s % 8, which takes a contiguous range of chains), so that the workgroups
         // sharing a chain's diagonal-block tiles share an L2 and few chains' panels are live in
         // the Infinity Cache at a time
-        const long rows = R - Kend, total = rows * nchains, L = blockIdx.x;
+        const long rows = R - row0, total = rows * nchains, L = blockIdx.x;
         const long xcd = L & 7, q = total >> 3, rm = total & 7;
         const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
         b = (int)(item / rows);
-        i = Kend + (int)(item % rows);
+        i = row0 + (int)(item % rows);
     } else {
         b = (int)(blockIdx.x % nchains);
         i = K + (int)(blockIdx.x / nchains);
@@ -459,8 +460,10 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) dacc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
     const float* Ai = Ab + (int64_t)(i * 64) * A.ld;
-    for (int k = K; k <= last; ++k) {
-        const int c = k - K;
+    // first column of the walk (BULK with a zero pattern: the row's first nonzero tile column)
+    const int kstart = (BULK && zrow > 0) ? max(K, zrow - 1 - i) : K;
+    for (int k = kstart; k <= last; ++k) {
+        const int c = k - kstart;
         DF_STAMP(0);
         float* Aik = Ab + (int64_t)(i * 64) * A.ld + k * 64;
         f4_t acc[2][2];
@@ -496,13 +499,13 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                     tile_gemm_nt32<true>(acc, Ai + (k - 1) * 64, A.ld, Ai + (k - 1) * 64, A.ld,
                                          64, sm.g, Aik, A.ld);
             } else if (h3) {
-                tile_gemm_nt32<true, true>(acc, Ai + K * 64, A.ld,
-                                           Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c,
-                                           sm.g, Aik, A.ld);
+                tile_gemm_nt32<true, true>(acc, Ai + kstart * 64, A.ld,
+                                           Ab + (int64_t)(k * 64) * A.ld + kstart * 64, A.ld,
+                                           64 * c, sm.g, Aik, A.ld);
             } else {
-                tile_gemm_nt32<true>(acc, Ai + K * 64, A.ld,
-                                     Ab + (int64_t)(k * 64) * A.ld + K * 64, A.ld, 64 * c, sm.g,
-                                     Aik, A.ld);
+                tile_gemm_nt32<true>(acc, Ai + kstart * 64, A.ld,
+                                     Ab + (int64_t)(k * 64) * A.ld + kstart * 64, A.ld, 64 * c,
+                                     sm.g, Aik, A.ld);
             }
             if (!BULK && k + 1 == i) {  // next step is the diagonal tile: its columns K .. k-1 now
                 if (h3)
@@ -617,6 +620,223 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
                        0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base,
                        timeouts);
     return true;
+}
+
+// ----------------------------------------------------------- row-panel TRSM of the bulk rows
+// Rows below an outer panel whose diagonal block L11 is factored (tiles and their inverses final):
+// L_i,P = A_i,P L11^-T over the panel's tile columns P = [K, K + ncols), ncols <= RP_NC. The
+// dataflow walk (k_chol_panel_df32) solves a row left-looking, re-reading the row's earlier panel
+// tiles from memory at each of its ncols dependent column steps (~95 us per walk).
+// Here the workgroup keeps its row's panel tiles in registers (wave (wr, wc) holds its 32 x 32
+// quadrant of every tile: 8 x 16 accumulators) and works right-looking: per column k, the TRSM
+// x = A_ik inv(L_kk)^T (f32 MFMA, as the walk's) is stored and staged once in LDS (negated; split
+// hi/lo for fp16x3 rows), and every later tile of the row receives -x L_jk^T (L_jk from L2,
+// double-buffered through LDS, the next tile's load in flight during the current product). No
+// global re-reads of the row, one barrier per 64-deep update. The accumulation order differs
+// from the walk's (rank-64 steps instead of one product over the earlier columns): rounding-level
+// differences that the Newton loop's fp64 refinement absorbs.
+#define RP_NC RP_NCOLS
+union RPOp {
+    float f[2][64][LP32];
+    struct {
+        _Float16 h[2][64][LPH], l[2][64][LPH];
+    } x;
+};
+struct RowPanelSmem {
+    RPOp a;     // the A operand: A_ik (TRSM) or -L_ik (updates)
+    RPOp b[2];  // the B operand: inv(L_kk) (TRSM) or L_jk (updates), double-buffered
+};
+
+// acc += A B^T over one 64-deep operand pair (two 32-deep slices)
+__device__ __forceinline__ void rp_gemm(f4_t (&acc)[2][2], const RPOp& A, const RPOp& B, bool h3,
+                                        int wr, int wc, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+    if (h3) {
+#pragma unroll
+        for (int cur = 0; cur < 2; ++cur) {
+            h8_t ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                ah[x] = *reinterpret_cast<const h8_t*>(&A.x.h[cur][32 * wr + 16 * x + r16][8 * kq]);
+                al[x] = *reinterpret_cast<const h8_t*>(&A.x.l[cur][32 * wr + 16 * x + r16][8 * kq]);
+                bh[x] = *reinterpret_cast<const h8_t*>(&B.x.h[cur][32 * wc + 16 * x + r16][8 * kq]);
+                bl[x] = *reinterpret_cast<const h8_t*>(&B.x.l[cur][32 * wc + 16 * x + r16][8 * kq]);
+            }
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj) {
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int cur = 0; cur < 2; ++cur)
+#pragma unroll
+        for (int t = 0; t < KS32 / 4; ++t) {
+            float a[2], bb[2];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) a[bi] = A.f[cur][32 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) bb[bj] = B.f[cur][32 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj)
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj], acc[bi][bj], 0, 0, 0);
+        }
+}
+
+// a wave's 32 x 32 accumulator quadrant -> operand slice wc (rows 32 wr ..), times sgn; fp32 or
+// split into fp16 hi / lo
+__device__ __forceinline__ void rp_stage_acc(RPOp& O, const f4_t (&v)[2][2], float sgn, bool h3,
+                                             int wr, int wc, int lane) {
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 32 * wr + 16 * bi + F32_CROW(lane, r), col = 16 * bj + (lane & 15);
+                const float x = sgn * v[bi][bj][r];
+                if (h3) {
+                    const _Float16 hx = (_Float16)x;
+                    O.x.h[wc][row][col] = hx;
+                    O.x.l[wc][row][col] = (_Float16)(x - (float)hx);
+                } else {
+                    O.f[wc][row][col] = x;
+                }
+            }
+}
+
+// 64 x 64 row-major tile (ld) -> registers: thread tid holds pieces p = tid + 256 h (row p / 16,
+// columns 4 (p % 16) .. +3)
+__device__ __forceinline__ void rp_load(f4_t (&pc)[4], const float* T, int64_t ld, int tid) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int p = tid + 256 * h;
+        pc[h] = *reinterpret_cast<const f4_t*>(T + (int64_t)(p >> 4) * ld + 4 * (p & 15));
+    }
+}
+__device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[4], bool h3, int tid) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int p = tid + 256 * h, row = p >> 4, col = 4 * (p & 15), sl = col >> 5, c = col & 31;
+        if (h3) {
+            h4_t hi, lo;
+            split_h3(pc[h], hi, lo);
+            *reinterpret_cast<h4_t*>(&O.x.h[sl][row][c]) = hi;
+            *reinterpret_cast<h4_t*>(&O.x.l[sl][row][c]) = lo;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) O.f[sl][row][c + e] = pc[h][e];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void k_panel_rows32(MatF A, int K, int ncols, int row0, int R,
+                                                         int zrow, int nchains,
+                                                         const float* __restrict__ Dinv,
+                                                         int64_t dstride, Live live, int hlim,
+                                                         const int* __restrict__ h3ok) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
+    // XCD-aware, chain-major (as the walk's BULK mapping): one chain's rows share an L2
+    const long rows = R - row0, total = rows * nchains, L = blockIdx.x;
+    const long xcd = L & 7, q = total >> 3, rm = total & 7;
+    const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
+    const int b = (int)(item / rows), i = row0 + (int)(item % rows);
+    if (!live32(live, b)) return;
+    const int kst = zrow > 0 ? max(0, zrow - 1 - i - K) : 0;  // first nonzero panel column
+    if (kst >= ncols) return;
+    __shared__ RowPanelSmem sm;
+    float* Ab = A.base + b * A.cstride;
+    float* Ai = Ab + (int64_t)(i * 64) * A.ld;
+    const float* Db = Dinv + b * dstride;
+    const bool h3 = i < hlim && (!h3ok || h3ok[b]);
+    f4_t acc[RP_NC][2][2];
+#pragma unroll
+    for (int kk = 0; kk < RP_NC; ++kk)
+        if (kk >= kst && kk < ncols) tile32_load(acc[kk], Ai + (K + kk) * 64, A.ld, wr, wc, lane);
+    auto get = [&](int j, f4_t (&t)[2][2]) {
+        switch (j) {
+#define RP_CASE(J) \
+    case J:        \
+        for (int x = 0; x < 2; ++x)   \
+            for (int y = 0; y < 2; ++y) t[x][y] = acc[J][x][y]; \
+        break;
+            RP_CASE(0) RP_CASE(1) RP_CASE(2) RP_CASE(3) RP_CASE(4) RP_CASE(5) RP_CASE(6) RP_CASE(7)
+#undef RP_CASE
+        }
+    };
+    auto put = [&](int j, const f4_t (&t)[2][2]) {
+        switch (j) {
+#define RP_CASE(J) \
+    case J:        \
+        for (int x = 0; x < 2; ++x)   \
+            for (int y = 0; y < 2; ++y) acc[J][x][y] = t[x][y]; \
+        break;
+            RP_CASE(0) RP_CASE(1) RP_CASE(2) RP_CASE(3) RP_CASE(4) RP_CASE(5) RP_CASE(6) RP_CASE(7)
+#undef RP_CASE
+        }
+    };
+    f4_t pre[4];
+    rp_load(pre, Db + (int64_t)(K + kst) * 4096, 64, tid);  // inv(L_kk) of the first column
+    for (int kk = kst; kk < ncols; ++kk) {
+        const int k = K + kk;
+        f4_t t[2][2], x[2][2];
+        get(kk, t);
+        // TRSM x = A_ik inv(L_kk)^T on f32 MFMA (k_chol_panel32's product)
+        rp_stage_acc(sm.a, t, 1.0f, false, wr, wc, lane);
+        rp_stage(sm.b[0], pre, false, tid);
+        __syncthreads();
+        if (kk + 1 < ncols) rp_load(pre, Ab + (int64_t)((K + kk + 1) * 64) * A.ld + k * 64, A.ld, tid);
+#pragma unroll
+        for (int x0 = 0; x0 < 2; ++x0)
+#pragma unroll
+            for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
+        rp_gemm(x, sm.a, sm.b[0], false, wr, wc, lane);
+        tile32_store(x, Ai + k * 64, A.ld, wr, wc, lane);
+        __syncthreads();
+        if (kk + 1 >= ncols) break;
+        // updates of the row's later tiles: acc_j -= x L_jk^T
+        rp_stage_acc(sm.a, x, -1.0f, h3, wr, wc, lane);
+        rp_stage(sm.b[0], pre, h3, tid);
+        __syncthreads();
+        int cur = 0;
+        for (int jj = kk + 1; jj < ncols; ++jj) {
+            // next operand in flight: L_(j+1)k, or inv(L_(k+1)(k+1)) after the last update
+            if (jj + 1 < ncols)
+                rp_load(pre, Ab + (int64_t)((K + jj + 1) * 64) * A.ld + k * 64, A.ld, tid);
+            else
+                rp_load(pre, Db + (int64_t)(k + 1) * 4096, 64, tid);
+            get(jj, t);
+            rp_gemm(t, sm.a, sm.b[cur], h3, wr, wc, lane);
+            put(jj, t);
+            if (jj + 1 < ncols) rp_stage(sm.b[cur ^ 1], pre, h3, tid);
+            __syncthreads();
+            cur ^= 1;
+        }
+    }
+}
+
+void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, const float* Dinv,
+                         int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
+                         hipStream_t s) {
+    if (ncols < 1 || R <= row0) return;
+    hipLaunchKernelGGL(k_panel_rows32, dim3((unsigned)((long)(R - row0) * nchains)), dim3(256), 0,
+                       s, A, K, ncols, row0, R, zrow, nchains, Dinv, dstride, live, hlim, h3ok);
+}
+
+void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
+                              FusedDiag<float> fd, Live live, int nchains, int hlim,
+                              const int* h3ok, hipStream_t s) {
+    if (ncols < 1 || R <= row0) return;
+    hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
+                       dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
+                       (int64_t)0, 0ull, nullptr, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update

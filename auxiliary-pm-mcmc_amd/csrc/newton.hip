@@ -265,12 +265,13 @@ void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet
 // mode 1 (PriorMC):       L = K_chol (A top-left), row np of L = 0
 // mode 2 (IS, chol(K)):   L = (block at rows np.., cols 0..) J, row np = g^T (vector v.Kb)
 // Rows are written whole (upper part zero) because the u-path GEMM streams full row segments.
+// mode 3 (IS, fp32 bottom): L = (rows np.. of S32) J, row np = g^T
 __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
                                                       const int64_t* __restrict__ slots, int mode,
                                                       int np, const double* __restrict__ gvec,
-                                                      int64_t gstride, Live live) {
+                                                      int64_t gstride, Live live, MatF S32) {
     const int b = blockIdx.y;
-    if (live.status[b] != 0) return;
+    if (live.status[b] != 0 || live.active[b] == 0) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = blockIdx.x * 4 + w;  // 0 .. np+63
     const double* Ab = A.base + b * A.cstride;
@@ -279,7 +280,14 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     // rows stop at the end of their diagonal tile: k_ugemm reads row r up to column
     // 64 (r / 64 + 1) only (apm_slot_read zeroes the rest on the host)
     const int cend = (r / 64 + 1) * 64;
-    if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
+    if (r < np && mode == 3) {  // as mode 2, from the fp32 bottom block
+        const float* src = S32.base + b * S32.cstride + ((int64_t)np + r) * S32.ld;
+        for (int c = lane; c < cend; c += 64) {
+            const float x = (c <= r) ? src[np - 1 - c] : 0.0f;
+            L[c] = x;
+            q += (double)x * (double)x;
+        }
+    } else if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
         const double* src = Ab + ((int64_t)np + r) * A.ld;
         for (int c = lane; c < cend; c += 64) {
             const double x = (c <= r) ? src[np - 1 - c] : 0.0;
@@ -293,7 +301,7 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
             L[c] = (float)x;
             q += x * x;
         }
-    } else if (r == np && mode == 2) {
+    } else if (r == np && mode >= 2) {
         const double* g = gvec + b * gstride;
         for (int c = lane; c < np; c += 64) L[c] = (float)g[c];
     } else {
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(256) void k_slot_write_L64(MatB A, SlotSet S,
                                                         const int64_t* __restrict__ slots,
                                                         int mode, int np, Live live) {
     const int b = blockIdx.y;
-    if (live.status[b] != 0 || !S.wide[slots[b]]) return;
+    if (live.status[b] != 0 || live.active[b] == 0 || !S.wide[slots[b]] || mode == 3) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = blockIdx.x * 4 + w;  // 0 .. np-1
     const double* Ab = A.base + b * A.cstride;
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
                                                         int mode, int n, Live live) {
     (void)A;
     const int b = blockIdx.x;
-    if (live.status[b] != 0) return;
+    if (live.status[b] != 0 || live.active[b] == 0) return;
     __shared__ double red[4];
     const int64_t np = (int64_t)nb * 64;
     const int64_t so = slots[b] * S.vstride;
@@ -355,9 +363,10 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
     __syncthreads();
     tq = block_sum_d(tq, red);
     if (threadIdx.x == 0) {
-        const int wd = tq > S.wide_q ? 1 : 0;
+        // (an fp32 bottom block above post_q is recomputed in fp64 and rewritten in mode 2)
+        const int wd = tq > S.wide_q && mode != 3 ? 1 : 0;
         S.wide[slots[b]] = wd;
-        S.chain_wide[b] = wd;
+        S.chain_wide[b] = wd | (mode == 3 && tq > S.post_q ? 2 : 0);
         double c = 0.0;
         if (mode != 1) {
             double ld = 0.0;
@@ -370,9 +379,9 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
 
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
-                       int nchains, hipStream_t s) {
+                       int nchains, hipStream_t s, MatF S32) {
     hipLaunchKernelGGL(k_slot_write_L, dim3((np + 64) / 4, nchains), dim3(256), 0, s, A, S, slots,
-                       mode, np, v.Kb, v.vstride, live);
+                       mode, np, v.Kb, v.vstride, live, S32);
     hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
     hipLaunchKernelGGL(k_slot_write_L64, dim3(np / 4, nchains), dim3(256), 0, s, A, S, slots, mode,

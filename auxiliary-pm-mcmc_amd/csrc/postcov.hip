@@ -254,6 +254,63 @@ void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t v
     }
 }
 
+// fp32 working copy for the posterior factor's bottom block (apm_internal.h). Grid x per chain:
+// [0, T) the top's tiles (i, j), j in [k0, k1), i >= j (rectangular index, upper ones skipped),
+// [T, T + k1 - k0) the diagonal-tile inverses of those columns, then (bottom) the bottom's tiles
+// (I, k), those before the outer panel of the row's first nonzero tile column nb - 1 - I skipped
+// (never read by the bottom's walks and updates).
+__global__ __launch_bounds__(256) void k_post32_convert(MatB A, MatF S, const double* __restrict__ D64,
+                                                        int64_t d64stride, float* __restrict__ D32,
+                                                        int64_t d32stride, int nb, int outer,
+                                                        int k0, int k1, Live live) {
+    const int b = blockIdx.y;
+    if (!live_pc(live, b)) return;
+    const int nc = k1 - k0, T = (nb - k0) * nc;
+    const int t = blockIdx.x;
+    const double* src;
+    int64_t sld;
+    float* dst;
+    int64_t dld;
+    if (t < T) {
+        const int ti = k0 + t / nc, tj = k0 + t % nc;
+        if (tj > ti) return;
+        src = A.base + b * A.cstride + (int64_t)(ti * 64) * A.ld + tj * 64;
+        sld = A.ld;
+        dst = S.base + b * S.cstride + (int64_t)(ti * 64) * S.ld + tj * 64;
+        dld = S.ld;
+    } else if (t < T + nc) {
+        const int k = k0 + t - T;
+        src = D64 + b * d64stride + (int64_t)k * 4096;
+        sld = 64;
+        dst = D32 + b * d32stride + (int64_t)k * 4096;
+        dld = 64;
+    } else {
+        const int u = t - T - nc, I = u / nb, k = u % nb;
+        const int kz = nb - 1 - I;  // first nonzero tile column of bottom row tile I
+        if (k < (kz / outer) * outer) return;
+        src = A.base + b * A.cstride + (int64_t)((nb + I) * 64) * A.ld + k * 64;
+        sld = A.ld;
+        dst = S.base + b * S.cstride + (int64_t)((nb + I) * 64) * S.ld + k * 64;
+        dld = S.ld;
+    }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
+        const d2_t v = *reinterpret_cast<const d2_t*>(src + (int64_t)r * sld + c);
+        *reinterpret_cast<f2_t*>(dst + (int64_t)r * dld + c) = f2_t{(float)v.x, (float)v.y};
+    }
+}
+
+void launch_post32_convert(MatB A, MatF S32, const double* D64, int64_t d64stride, float* D32,
+                           int64_t d32stride, int nb, int outer, int k0, int k1, bool bottom,
+                           Live live, int nchains, hipStream_t s) {
+    const int nc = k1 - k0, T = (nb - k0) * nc;
+    const int grid = T + nc + (bottom ? nb * nb : 0);
+    if (grid <= 0) return;
+    hipLaunchKernelGGL(k_post32_convert, dim3(grid, nchains), dim3(256), 0, s, A, S32, D64,
+                       d64stride, D32, d32stride, nb, outer, k0, k1, live);
+}
+
 __global__ void k_merge_status(int* status, const int* other, int code, int nchains) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nchains && other[b] != 0) status[b] = code;

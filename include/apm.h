@@ -134,7 +134,11 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
                                  factorisation's dataflow panel launches (each fails its chain,
                                  which the Newton loop reruns in fp64; apart from breakdowns of
                                  the fp32 factor, which are not counted here) */
-#define APM_PROF_NKINDS 8
+#define APM_PROF_POST32_OUTER 8 /* the rank-64*OUTER trailing updates of the posterior factor's
+                                   bottom block in fp32 (postcov.hip, APM_POST32) */
+#define APM_PROF_POST64_RERUNS 9 /* not a kernel: launches = chains whose posterior bottom block was
+                                    recomputed in fp64 (trace of C above the fp32 bound) */
+#define APM_PROF_NKINDS 10
 /* on = 0 off; 1 the roofline kinds (GRAM, UGEMM and the two *_OUTER kinds: one event pair per
  * launch of those kernels only, so that the timing adds little to a timed region); 2 every kind
  * (CHOL_UPDATE / CHOL_UPDATE32 add an event pair around every in-panel update launch) */

@@ -332,27 +332,90 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
         assert ob1[b] == o1[b]
 
 
+def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
+    """_run_is plus the slots' factors and the fp64-rerun counter of the posterior bottom block."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    B = len(thetas)
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, ns.shape[1], max_batch=B, n_slots=B, n_ubufs=1)
+    for k in env:
+        monkeypatch.delenv(k)
+    ctx.u_upload(0, ns)
+    ctx.prof_read(nat.PROF_POST64_RERUNS, reset=True)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, thetas, ubufs=[0] * B, slots=list(range(B)))
+    reruns = ctx.prof_read(nat.PROF_POST64_RERUNS, reset=True)[1]
+    u_out, u_st = ctx.u_eval(list(range(B)), [0] * B)
+    rd = [ctx.slot_read(b) for b in range(B)]
+    ctx.close()
+    return out, st, nops, rd, reruns, u_out
+
+
+@pytest.mark.parametrize('n', [700, 1100])
+def test_posterior_bottom_fp32_matches_fp64(nat, monkeypatch, n):
+    """The posterior factor's bottom block (L_K J) L'^-T in fp32 (default: beside the fp64
+    factorisation of J M J on the second stream, APM_POST32=1: after it; postcov.hip) against
+    the all-fp64 stacked factorisation (APM_POST32=0): Newton modes and log|B| untouched (bitwise
+    equal f_post and cst), chol(C) within fp32 accuracy of its maximum, estimates within 1e-4
+    nats (the fp32 TRSM moves log f by ~1e-9 x trace(C)). n = 1100: a ragged last outer panel.
+    Also the fp64 recomputation of the chains above the trace bound (APM_POST32_Q=0: all of them)
+    against the all-fp64 path: fp64 either way, to 1e-9 relative."""
+    X, y, thetas, ns = _mixed_case(n=n)
+    o0, s0, n0, r0, k0, u0 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32=0)
+    o1, s1, n1, r1, k1, u1 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch)
+    o2, s2, n2, r2, k2, u2 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32_Q=0)
+    # the bottom block after the fp64 factorisation instead of beside it: the same kernels on the
+    # same operands, bitwise
+    o3, s3, n3, r3, k3, u3 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32=1)
+    np.testing.assert_array_equal(o3, o1)
+    np.testing.assert_array_equal(u3, u1)
+    for b in range(len(thetas)):
+        np.testing.assert_array_equal(r3[b][0], r1[b][0])
+    assert (s0 == 0).all() and (s1 == 0).all() and (s2 == 0).all()
+    np.testing.assert_array_equal(n1, n0)
+    assert k0 == 0 and k2 == len(thetas)
+    for b in range(len(thetas)):
+        L0, f0, g0, c0 = r0[b]
+        L1, f1, g1, c1 = r1[b]
+        np.testing.assert_array_equal(f1, f0)
+        assert c1 == c0
+        assert np.abs(L1 - L0).max() <= 1e-5 * np.abs(L0).max(), (b, np.abs(L1 - L0).max())
+        assert abs(o1[b] - o0[b]) <= 1e-4, (b, o1[b], o0[b])
+        assert abs(u1[b] - u0[b]) <= 1e-4, (b, u1[b], u0[b])
+        L2 = r2[b][0]
+        assert np.abs(L2 - L0).max() <= 1e-6 * np.abs(L0).max()
+        assert abs(o2[b] - o0[b]) <= 1e-9 * max(1.0, abs(o0[b])), (b, o2[b], o0[b])
+
+
 @pytest.mark.parametrize('n', [560, 1100])
 def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch, n):
-    """The Newton factor's in-panel steps as one dataflow launch per outer panel
-    (k_chol_panel_df32, default) against the per-column launch sequence (APM_DF32=0): same
-    operands, same accumulation order, so modes, estimates, statuses and iteration counts are
-    bitwise equal - also for a batch with a chain at an extreme theta (fp32 operands, possibly a
-    failed fp32 factorisation and its fp64 rerun) next to ordinary ones; n = 560: a last outer
-    panel of one column (its TRSM only), n = 1100: three outer panels."""
+    """The Newton factor's in-panel steps. APM_DF32=1, one dataflow launch per outer panel whose
+    rows walk the panel's columns (k_chol_panel_df32), against the per-column launch sequence
+    (APM_DF32=0): same operands, same accumulation order, so modes, estimates, statuses and
+    iteration counts are bitwise equal - also for a batch with a chain at an extreme theta (fp32
+    operands, possibly a failed fp32 factorisation and its fp64 rerun) next to ordinary ones.
+    Default (2): the dataflow chain for the diagonal block, then the rows below it right-looking
+    with their panel tiles in registers (k_panel_rows32): a different accumulation order, so the
+    same statuses and iteration counts, modes within 1e-9 relative and estimates within 1e-6.
+    n = 560: a last outer panel of one column (its TRSM only), n = 1100: three outer panels, the
+    last of two columns."""
     X, y, thetas, ns = _mixed_case(n=n)
     ext = thetas[0].copy()
     ext[0] = 45.0
     thetas = np.vstack([thetas, ext])
     o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0)
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=1)
+    o2, s2, n2, f2 = _run_is(nat, X, y, thetas, ns, monkeypatch)
     np.testing.assert_array_equal(s1, s0)
     np.testing.assert_array_equal(n1, n0)
+    np.testing.assert_array_equal(s2, s0)
+    np.testing.assert_array_equal(n2, n0)
     assert (s0[:3] == 0).all()
     for b in range(len(thetas)):
         if s0[b] == 0:
             np.testing.assert_array_equal(f1[b], f0[b])
             assert o1[b] == o0[b]
+            np.testing.assert_allclose(f2[b], f0[b], rtol=1e-9, atol=1e-9 * np.abs(f0[b]).max())
+            assert abs(o2[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o2[b], o0[b])
 
 
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
