@@ -457,13 +457,14 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
         self._rd_next(c)
         return False
 
-    def run_async(self, n_steps, keep_going=False):
+    def run_async(self, n_steps, keep_going=False, on_round=None):
         """Advance every live chain by at least ``n_steps`` transitions (a number, or one per
         chain) with the asynchronous schedule. keep_going=False: a chain stops after n_steps
         (the call ends with every chain at a transition boundary); True: chains that are ahead keep working until the slowest
         has n_steps (throughput mode; a final partial transition is discarded).
         Returns (traces, done): per chain the list of thetas after each completed transition and
-        the number of completed transitions."""
+        the number of completed transitions. on_round(done): called after every batched
+        theta-call (progress reporting)."""
         C = self.n_chains
         n_steps = np.broadcast_to(np.asarray(n_steps, dtype=np.int64), (C,))  # or per chain
         done = np.zeros(C, dtype=np.int64)
@@ -494,6 +495,8 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
                         done[c] += 1
                         traces[c].append(self.theta[c].copy())
                         need_u[c] = True
+            if on_round is not None:
+                on_round(done)
         return traces, done
 
     def run(self, n_steps, theta_init=None, warmup_callback=None):

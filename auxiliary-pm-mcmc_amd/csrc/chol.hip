@@ -174,6 +174,135 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 // Stand-alone diag step (one wave per chain): tile (k, k) -> LDS, diag_compute + diag_store (diag.h). Used for
 // the first column of every factorisation; every later diagonal tile is factored inside the
 // update launch that produces it (k_chol_update below, fuse_diag).
+// ----------------------------------------------------------- row-panel TRSM of the bulk rows (fp64)
+// The fp64 twin of chol32.hip's k_panel_rows32: rows [row0, R) below an outer panel whose
+// diagonal block L11 is factored get L_i,P = A_i,P L11^-T over the panel's tile columns
+// P = [K, K + ncols) (ncols <= RP_NCOLS) in one launch, right-looking inside the workgroup with the
+// row's panel tiles in registers (8 waves, wave w owns 16 x 32 of every tile: 2 accumulators of
+// v_mfma_f64_16x16x4_f64 per tile), instead of the per-column launch pairs (left-looking update,
+// then panel TRSM) over all rows, whose updates re-read the row's earlier panel tiles (DESIGN.md
+// §5: ~25 % of the fp64 peak in those launches). Per column k: x = A_ik inv(L_kk)^T (stored, and
+// staged in LDS negated), then every later tile of the row receives -x L_jk^T (L_jk from L2,
+// double-buffered, the next one's load in flight). zrow > 0: row tile i is zero before tile
+// column zrow - 1 - i (the stacked posterior factorisation's L_K J).
+#define RP64_NC RP_NCOLS
+#define RPP 65  // LDS pitch (doubles)
+struct RowPanelSmem64 {
+    double a[64][RPP];
+    double b[2][64][RPP];
+};
+
+__device__ __forceinline__ void rp64_gemm(d4_t (&acc)[2], const double (*A)[RPP], const double (*B)[RPP],
+                                          int br, int bc0, int lane) {
+    const int r16 = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+    for (int t = 0; t < 16; ++t) {
+        const double a = A[16 * br + r16][4 * t + kq];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, B[16 * (bc0 + j) + r16][4 * t + kq],
+                                                          acc[j], 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void rp64_stage_acc(double (*A)[RPP], const d4_t (&v)[2], double sgn,
+                                               int br, int bc0, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            A[16 * br + F64_CROW(lane, r)][16 * (bc0 + j) + (lane & 15)] = sgn * v[j][r];
+}
+__device__ __forceinline__ void rp64_load(d2_t (&pc)[4], const double* T, int64_t ld, int tid) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int p = tid + 512 * h;
+        pc[h] = *reinterpret_cast<const d2_t*>(T + (int64_t)(p >> 5) * ld + 2 * (p & 31));
+    }
+}
+__device__ __forceinline__ void rp64_stage(double (*B)[RPP], const d2_t (&pc)[4], int tid) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const int p = tid + 512 * h, row = p >> 5, col = 2 * (p & 31);
+        B[row][col] = pc[h].x;
+        B[row][col + 1] = pc[h].y;
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void k_panel_rows64(MatB A, int K, int ncols, int row0, int R,
+                                                         int zrow, int nchains,
+                                                         const double* __restrict__ Dinv,
+                                                         int64_t dstride, Live live) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, br = wv >> 1, bc0 = 2 * (wv & 1);
+    const long rows = R - row0, total = rows * nchains, L = blockIdx.x;
+    const long xcd = L & 7, q = total >> 3, rm = total & 7;
+    const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
+    const int b = (int)(item / rows), i = row0 + (int)(item % rows);
+    if (!chain_live(live, b)) return;
+    const int kst = zrow > 0 ? max(0, zrow - 1 - i - K) : 0;
+    if (kst >= ncols) return;
+    __shared__ RowPanelSmem64 sm;
+    double* Ab = A.base + b * A.cstride;
+    double* Ai = Ab + (int64_t)(i * 64) * A.ld;
+    const double* Db = Dinv + b * dstride;
+    d4_t acc[RP64_NC][2];  // register resident: compile-time indices only (unrolled loops)
+    auto tload = [&](d4_t (&v)[2], const double* T) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                v[j][r] = T[(int64_t)(16 * br + F64_CROW(lane, r)) * A.ld + 16 * (bc0 + j) + (lane & 15)];
+    };
+    auto tstore = [&](const d4_t (&v)[2], double* T) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                T[(int64_t)(16 * br + F64_CROW(lane, r)) * A.ld + 16 * (bc0 + j) + (lane & 15)] = v[j][r];
+    };
+#pragma unroll
+    for (int kk = 0; kk < RP64_NC; ++kk)
+        if (kk >= kst && kk < ncols) tload(acc[kk], Ai + (K + kk) * 64);
+    d2_t pre[4];
+    rp64_load(pre, Db + (int64_t)(K + kst) * 4096, 64, tid);
+#pragma unroll
+    for (int kk = 0; kk < RP64_NC; ++kk) {
+        if (kk < kst || kk >= ncols) continue;
+        const int k = K + kk;
+        rp64_stage_acc(sm.a, acc[kk], 1.0, br, bc0, lane);  // TRSM x = A_ik inv(L_kk)^T
+        rp64_stage(sm.b[0], pre, tid);
+        __syncthreads();
+        if (kk + 1 < ncols) rp64_load(pre, Ab + (int64_t)((K + kk + 1) * 64) * A.ld + k * 64, A.ld, tid);
+        d4_t x[2];
+        x[0] = x[1] = d4_t{0.0, 0.0, 0.0, 0.0};
+        rp64_gemm(x, sm.a, sm.b[0], br, bc0, lane);
+        tstore(x, Ai + k * 64);
+        __syncthreads();
+        if (kk + 1 >= ncols) break;
+        rp64_stage_acc(sm.a, x, -1.0, br, bc0, lane);  // updates: acc_j -= x L_jk^T
+        rp64_stage(sm.b[0], pre, tid);
+        __syncthreads();
+#pragma unroll
+        for (int jj = kk + 1; jj < RP64_NC; ++jj) {
+            if (jj >= ncols) break;
+            const int cur = (jj - kk - 1) & 1;
+            if (jj + 1 < ncols)
+                rp64_load(pre, Ab + (int64_t)((K + jj + 1) * 64) * A.ld + k * 64, A.ld, tid);
+            else
+                rp64_load(pre, Db + (int64_t)(k + 1) * 4096, 64, tid);
+            rp64_gemm(acc[jj], sm.a, sm.b[cur], br, bc0, lane);
+            if (jj + 1 < ncols) rp64_stage(sm.b[cur ^ 1], pre, tid);
+            __syncthreads();
+        }
+    }
+}
+
+void launch_panel_rows64(MatB A, int K, int ncols, int row0, int R, int zrow, const double* Dinv,
+                         int64_t dstride, Live live, int nchains, hipStream_t s) {
+    if (ncols < 1 || R <= row0) return;
+    hipLaunchKernelGGL(k_panel_rows64, dim3((unsigned)((long)(R - row0) * nchains)), dim3(512), 0,
+                       s, A, K, ncols, row0, R, zrow, nchains, Dinv, dstride, live);
+}
+
 template <class Mat, class TS>
 __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_t dstride,
                                                   double* ldet, int64_t lstride, Live live,

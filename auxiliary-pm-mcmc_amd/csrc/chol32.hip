@@ -737,6 +737,7 @@ __device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[4], bool h3, 
     }
 }
 
+template <bool H3>
 __global__ __launch_bounds__(256, 2) void k_panel_rows32(MatF A, int K, int ncols, int row0, int R,
                                                          int zrow, int nchains,
                                                          const float* __restrict__ Dinv,
@@ -749,50 +750,33 @@ __global__ __launch_bounds__(256, 2) void k_panel_rows32(MatF A, int K, int ncol
     const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
     const int b = (int)(item / rows), i = row0 + (int)(item % rows);
     if (!live32(live, b)) return;
+    // fp16x3 operands in the updates of rows below hlim of the chains h3ok allows; the two kinds
+    // of rows are two launches of this kernel (H3 a template parameter: one code path each)
+    if ((i < hlim && (!h3ok || h3ok[b])) != H3) return;
     const int kst = zrow > 0 ? max(0, zrow - 1 - i - K) : 0;  // first nonzero panel column
     if (kst >= ncols) return;
     __shared__ RowPanelSmem sm;
     float* Ab = A.base + b * A.cstride;
     float* Ai = Ab + (int64_t)(i * 64) * A.ld;
     const float* Db = Dinv + b * dstride;
-    const bool h3 = i < hlim && (!h3ok || h3ok[b]);
+    // the row's panel tiles, register resident: every index below is a compile-time constant
+    // (fully unrolled loops with uniform run-time guards), so nothing goes to scratch
     f4_t acc[RP_NC][2][2];
 #pragma unroll
     for (int kk = 0; kk < RP_NC; ++kk)
         if (kk >= kst && kk < ncols) tile32_load(acc[kk], Ai + (K + kk) * 64, A.ld, wr, wc, lane);
-    auto get = [&](int j, f4_t (&t)[2][2]) {
-        switch (j) {
-#define RP_CASE(J) \
-    case J:        \
-        for (int x = 0; x < 2; ++x)   \
-            for (int y = 0; y < 2; ++y) t[x][y] = acc[J][x][y]; \
-        break;
-            RP_CASE(0) RP_CASE(1) RP_CASE(2) RP_CASE(3) RP_CASE(4) RP_CASE(5) RP_CASE(6) RP_CASE(7)
-#undef RP_CASE
-        }
-    };
-    auto put = [&](int j, const f4_t (&t)[2][2]) {
-        switch (j) {
-#define RP_CASE(J) \
-    case J:        \
-        for (int x = 0; x < 2; ++x)   \
-            for (int y = 0; y < 2; ++y) acc[J][x][y] = t[x][y]; \
-        break;
-            RP_CASE(0) RP_CASE(1) RP_CASE(2) RP_CASE(3) RP_CASE(4) RP_CASE(5) RP_CASE(6) RP_CASE(7)
-#undef RP_CASE
-        }
-    };
     f4_t pre[4];
     rp_load(pre, Db + (int64_t)(K + kst) * 4096, 64, tid);  // inv(L_kk) of the first column
-    for (int kk = kst; kk < ncols; ++kk) {
+#pragma unroll
+    for (int kk = 0; kk < RP_NC; ++kk) {
+        if (kk < kst || kk >= ncols) continue;
         const int k = K + kk;
-        f4_t t[2][2], x[2][2];
-        get(kk, t);
         // TRSM x = A_ik inv(L_kk)^T on f32 MFMA (k_chol_panel32's product)
-        rp_stage_acc(sm.a, t, 1.0f, false, wr, wc, lane);
+        rp_stage_acc(sm.a, acc[kk], 1.0f, false, wr, wc, lane);
         rp_stage(sm.b[0], pre, false, tid);
         __syncthreads();
         if (kk + 1 < ncols) rp_load(pre, Ab + (int64_t)((K + kk + 1) * 64) * A.ld + k * 64, A.ld, tid);
+        f4_t x[2][2];
 #pragma unroll
         for (int x0 = 0; x0 < 2; ++x0)
 #pragma unroll
@@ -802,22 +786,21 @@ __global__ __launch_bounds__(256, 2) void k_panel_rows32(MatF A, int K, int ncol
         __syncthreads();
         if (kk + 1 >= ncols) break;
         // updates of the row's later tiles: acc_j -= x L_jk^T
-        rp_stage_acc(sm.a, x, -1.0f, h3, wr, wc, lane);
-        rp_stage(sm.b[0], pre, h3, tid);
+        rp_stage_acc(sm.a, x, -1.0f, H3, wr, wc, lane);
+        rp_stage(sm.b[0], pre, H3, tid);
         __syncthreads();
-        int cur = 0;
-        for (int jj = kk + 1; jj < ncols; ++jj) {
+#pragma unroll
+        for (int jj = kk + 1; jj < RP_NC; ++jj) {
+            if (jj >= ncols) break;
+            const int cur = (jj - kk - 1) & 1;
             // next operand in flight: L_(j+1)k, or inv(L_(k+1)(k+1)) after the last update
             if (jj + 1 < ncols)
                 rp_load(pre, Ab + (int64_t)((K + jj + 1) * 64) * A.ld + k * 64, A.ld, tid);
             else
                 rp_load(pre, Db + (int64_t)(k + 1) * 4096, 64, tid);
-            get(jj, t);
-            rp_gemm(t, sm.a, sm.b[cur], h3, wr, wc, lane);
-            put(jj, t);
-            if (jj + 1 < ncols) rp_stage(sm.b[cur ^ 1], pre, h3, tid);
+            rp_gemm(acc[jj], sm.a, sm.b[cur], H3, wr, wc, lane);
+            if (jj + 1 < ncols) rp_stage(sm.b[cur ^ 1], pre, H3, tid);
             __syncthreads();
-            cur ^= 1;
         }
     }
 }
@@ -826,8 +809,12 @@ void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, co
                          int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
                          hipStream_t s) {
     if (ncols < 1 || R <= row0) return;
-    hipLaunchKernelGGL(k_panel_rows32, dim3((unsigned)((long)(R - row0) * nchains)), dim3(256), 0,
-                       s, A, K, ncols, row0, R, zrow, nchains, Dinv, dstride, live, hlim, h3ok);
+    const dim3 grid((unsigned)((long)(R - row0) * nchains));
+    if (hlim > row0)
+        hipLaunchKernelGGL(k_panel_rows32<true>, grid, dim3(256), 0, s, A, K, ncols, row0, R, zrow,
+                           nchains, Dinv, dstride, live, hlim, h3ok);
+    hipLaunchKernelGGL(k_panel_rows32<false>, grid, dim3(256), 0, s, A, K, ncols, row0, R, zrow,
+                       nchains, Dinv, dstride, live, hlim, h3ok);
 }
 
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,

@@ -535,12 +535,11 @@ def ess_block(dist, smp, series, done, burn, elapsed, P):
 
 
 def ess_long_record(value, a):
-    """The long-chain ESS record of this workload (SURVEY.md §8d protocol: 500 warm-up
-    transitions discarded, 2000 kept per chain; tools/ess_long.py on one MI355X -> the newest
-    profiles/r*_ess_long.json): its ESS per transition (min over the theta components) x this
-    run's transitions/s. The in-run ess_per_sec above rests on 100-transition segments, where the
-    AR fit cannot see the slow modes of a 33-dimensional random-direction slice sampler, and
-    over-states the long-chain figure ~4x."""
+    """The long-chain ESS record of this workload (SURVEY.md §8d protocol, Analyse
+    results.ipynb:138-141: R-hat and ESS on long chains after a warm-up; tools/ess_long.py on one
+    MI355X -> the newest profiles/r*_ess_long.json): its ESS per transition (min and mean over the
+    theta components) x this run's transitions/s. This is the headline ESS/s: the in-run figure
+    rests on ~100-transition segments whose R-hat shows the chains have not mixed there."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_ess_long.json')))
     if not files:
@@ -550,12 +549,19 @@ def ess_long_record(value, a):
     if (cfg.get('n_data'), cfg.get('n_features'), cfg.get('n_imp')) != (a.n, a.d, a.n_imp):
         return None
     ept = r['ess_per_transition_min_component']
+    eptm = r.get('ess_per_transition_mean_component')
     return {'source': os.path.relpath(files[-1], REPO),
             'ess_per_transition_min_component': ept,
+            'ess_per_transition_mean_component': eptm,
             'ess_per_sec_estimate': ept * value,
-            'rhat_max': r['rhat_max'], 'chains': cfg.get('chains'),
-            'warmup_discarded': cfg.get('warmup_discarded'),
-            'kept_per_chain': cfg.get('kept_per_chain'),
+            'ess_mean_per_sec_estimate': eptm * value if eptm is not None else None,
+            'rhat_max': r['rhat_max'], 'rhat_median': r.get('rhat_median'),
+            'converged_rhat_below_1p1': r['rhat_max'] < 1.1,
+            'rhat_below_1p1_at_transitions_per_chain':
+                r.get('rhat_below_1p1_at_transitions_per_chain'),
+            'chains': cfg.get('chains'),
+            'warmup_discarded': r.get('warmup_discarded', cfg.get('warmup_discarded')),
+            'kept_per_chain': r.get('kept_per_chain', cfg.get('kept_per_chain')),
             'note': 'ESS per transition from the long-chain record x this run\'s transitions/s'}
 
 
@@ -639,10 +645,12 @@ def main():
     prof = {}
     for k, name in ((_native.PROF_GRAM, 'gram'), (_native.PROF_CHOL_UPDATE_OUTER, 'chol_update'),
                     (_native.PROF_UGEMM, 'ugemm'),
-                    (_native.PROF_CHOL_UPDATE32_OUTER, 'chol_update32')):
+                    (_native.PROF_CHOL_UPDATE32_OUTER, 'chol_update32'),
+                    (_native.PROF_POST32_OUTER, 'post32')):
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
     _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
+    _, n_post64, _ = ctx.prof_read(_native.PROF_POST64_RERUNS, reset=True)
     _, n_df_timeouts, _ = ctx.prof_read(_native.PROF_DF_TIMEOUTS, reset=True)
 
     def mfma_roofline(name, kernel, peak, shorts, kind):
@@ -676,10 +684,19 @@ def main():
                           ('k_chol_update32_t128<true, false>', 'k_chol_update32_t128<true, true>',
                            'k_chol_update32_t128<false, false>',  # round-2 names:
                            'k_chol_update32_t128<true>', 'k_chol_update32_t128<false>'), 'f16x3')
+    # the posterior factor's fp32 bottom block (same kernel as the Newton update, so its PMC
+    # traffic cannot be told apart in a counter pass: timing and flops only)
+    post32 = mfma_roofline('post32', 'k_chol_update32_t128 on the posterior factor\'s bottom block '
+                           '(L_K J) L\'^-T (fp32 / fp16x3, second stream; postcov.hip)',
+                           PEAK_F16X3_TFLOPS, (), 'f16x3')
+    if post32 is not None:
+        post32['traffic_note'] = 'shares its kernel with the Newton update: no separate PMC pass'
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])
     extra = {}
+    if post32 is not None:
+        extra['roofline_post32'] = post32
     for r, key in ((upd64, 'roofline_update_f64'), (upd32, 'roofline_update_f32')):
         if r is not None and r is not roofline:
             extra[key] = r
@@ -788,6 +805,8 @@ def main():
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
                    .format(dist.world)},
         'ess_per_sec': ess['ess_per_sec'], 'ess_mean_per_sec': ess['ess_mean_per_sec'],
+        'ess_per_sec_source': 'in-run sample (see ess_sample; replaced by the long-chain record '
+                              'when one exists)',
         'rhat': ess['rhat'], 'ess_sample': ess['sample'],
         'parity': parity,
         'schedule': a.schedule, 'transitions_timed': int(transitions),
@@ -795,6 +814,7 @@ def main():
         'failed_chains': failed,
         'newton_refinement_steps': int(dist.sum(n_refine)),
         'newton_fp64_reruns': int(dist.sum(n_rerun)),
+        'posterior_bottom_fp64_reruns': int(dist.sum(n_post64)),
         'newton_dataflow_spin_timeouts': int(dist.sum(n_df_timeouts)),
         'cubic_ops_per_theta_call': {
             'mean_of_batch_max': float(np.mean([m for m, _ in call_ops])) if call_ops else None,
@@ -809,7 +829,17 @@ def main():
     line.update(extra)
     # the PMC numbers (traffic, mfma_busy) come from a committed counter pass: of this build?
     line['pmc_provenance'] = pmc_provenance()
-    line['ess_long_chain'] = ess_long_record(value, a)
+    line['ess_long_chain'] = lr = ess_long_record(value, a)
+    if lr is not None:  # the headline ESS/s from mixed (or, if not yet, the longest) chains
+        line['ess_sample']['ess_per_sec_in_run'] = line['ess_per_sec']
+        line['ess_sample']['ess_mean_per_sec_in_run'] = line['ess_mean_per_sec']
+        line['ess_per_sec'] = lr['ess_per_sec_estimate']
+        line['ess_mean_per_sec'] = lr['ess_mean_per_sec_estimate']
+        line['ess_per_sec_source'] = (
+            'long-chain record {0}: ESS per transition (min over theta components) x this run\'s '
+            'transitions/s; R-hat max {1:.3f} ({2})'.format(
+                lr['source'], lr['rhat_max'],
+                'converged' if lr['converged_rhat_below_1p1'] else 'NOT converged: R-hat > 1.1'))
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     ok = parity is None or parity['pass']

@@ -133,14 +133,24 @@ def main():
     seg = [[] for _ in range(a.chains)]
     t0 = time.perf_counter()
     done_here = 0
-    while have + done_here < a.target and time.perf_counter() - t0 < a.max_seconds:
+    last = 0.0  # duration of the previous chunk: no chunk is started that would overrun
+    while have + done_here < a.target and time.perf_counter() - t0 + last < a.max_seconds:
+        tc = time.perf_counter()
         step = min(a.chunk, a.target - have - done_here)
-        tr, done = smp.run_async(step)
+        beat = [time.perf_counter()]
+
+        def heartbeat(done):  # a line a minute inside long chunks (gpurun's hang detection)
+            if time.perf_counter() - beat[0] > 60:
+                beat[0] = time.perf_counter()
+                print('  ... chunk: slowest chain {0} / {1}'.format(int(done.min()), step),
+                      file=sys.stderr, flush=True)
+        tr, done = smp.run_async(step, on_round=heartbeat)
         for c in range(a.chains):
             if smp.failed[c]:
                 tr[c] = tr[c] + [smp.theta[c].copy()] * (step - len(tr[c]))
             seg[c].extend(tr[c])
         done_here += step
+        last = time.perf_counter() - tc
         print('{0} / {1} transitions per chain, segment {2:.0f} s'.format(
             have + done_here, a.target, time.perf_counter() - t0), file=sys.stderr, flush=True)
     wall = time.perf_counter() - t0
