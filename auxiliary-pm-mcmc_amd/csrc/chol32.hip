@@ -625,17 +625,20 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
 // ----------------------------------------------------------- row-panel TRSM of the bulk rows
 // Rows below an outer panel whose diagonal block L11 is factored (tiles and their inverses final):
 // L_i,P = A_i,P L11^-T over the panel's tile columns P = [K, K + ncols), ncols <= RP_NC. The
-// dataflow walk (k_chol_panel_df32) solves a row left-looking, re-reading the row's earlier panel
+// dataflow walk (k_chol_panel_df32) solves a row left-looking and re-reads the row's earlier panel
 // tiles from memory at each of its ncols dependent column steps (~95 us per walk).
-// Here the workgroup keeps its row's panel tiles in registers (wave (wr, wc) holds its 32 x 32
-// quadrant of every tile: 8 x 16 accumulators) and works right-looking: per column k, the TRSM
-// x = A_ik inv(L_kk)^T (f32 MFMA, as the walk's) is stored and staged once in LDS (negated; split
-// hi/lo for fp16x3 rows), and every later tile of the row receives -x L_jk^T (L_jk from L2,
-// double-buffered through LDS, the next tile's load in flight during the current product). No
-// global re-reads of the row, one barrier per 64-deep update. The accumulation order differs
-// from the walk's (rank-64 steps instead of one product over the earlier columns): rounding-level
-// differences that the Newton loop's fp64 refinement absorbs.
+// Here a workgroup of RP_RW x 4 waves takes RP_RW rows of one chain; each row's panel tiles stay
+// in registers (wave (wr, wc) of the row's group holds its 32 x 32 quadrant of every tile) and the
+// row is solved right-looking: per column k, the TRSM x = (U_ik + A_ik) inv(L_kk)^T (f32 MFMA) is
+// stored and staged once in LDS (negated; hi/lo for fp16x3 rows), and every later tile's update sum
+// U_ij receives -x L_jk^T. The B operands - inv(L_kk) and the tiles L_jk of the diagonal block -
+// are the same for every row of the chain: they stream through LDS once per workgroup (shared by
+// its rows), two operands of global loads in flight ahead of the one multiplied. Accumulation is
+// in the walk's order (each U_ij sums its products from zero in column order, the old tile A_ij
+// is added before the TRSM, as tile_gemm_nt32 adds C after its products), so the factor is
+// bitwise the walk's.
 #define RP_NC RP_NCOLS
+#define RP_RW 2  // rows per workgroup
 union RPOp {
     float f[2][64][LP32];
     struct {
@@ -643,11 +646,12 @@ union RPOp {
     } x;
 };
 struct RowPanelSmem {
-    RPOp a;     // the A operand: A_ik (TRSM) or -L_ik (updates)
-    RPOp b[2];  // the B operand: inv(L_kk) (TRSM) or L_jk (updates), double-buffered
+    RPOp a[RP_RW];  // per row: the A operand, A_ik (TRSM) or -L_ik (updates)
+    RPOp b[2];      // the shared B operand, inv(L_kk) (TRSM) or L_jk (updates), double-buffered
 };
 
-// acc += A B^T over one 64-deep operand pair (two 32-deep slices)
+// acc += A B^T over one 64-deep operand pair (two 32-deep slices), the MFMA sequence of
+// tile_gemm_nt32 (fp16x3: hi.hi, hi.lo, lo.hi per 16x16x32 block)
 __device__ __forceinline__ void rp_gemm(f4_t (&acc)[2][2], const RPOp& A, const RPOp& B, bool h3,
                                         int wr, int wc, int lane) {
     const int r16 = lane & 15, kq = lane >> 4;
@@ -690,8 +694,7 @@ __device__ __forceinline__ void rp_gemm(f4_t (&acc)[2][2], const RPOp& A, const 
         }
 }
 
-// a wave's 32 x 32 accumulator quadrant -> operand slice wc (rows 32 wr ..), times sgn; fp32 or
-// split into fp16 hi / lo
+// a wave's 32 x 32 quadrant (times sgn) -> operand slice wc (rows 32 wr ..); fp32, or fp16 hi / lo
 __device__ __forceinline__ void rp_stage_acc(RPOp& O, const f4_t (&v)[2][2], float sgn, bool h3,
                                              int wr, int wc, int lane) {
 #pragma unroll
@@ -712,19 +715,21 @@ __device__ __forceinline__ void rp_stage_acc(RPOp& O, const f4_t (&v)[2][2], flo
             }
 }
 
-// 64 x 64 row-major tile (ld) -> registers: thread tid holds pieces p = tid + 256 h (row p / 16,
-// columns 4 (p % 16) .. +3)
-__device__ __forceinline__ void rp_load(f4_t (&pc)[4], const float* T, int64_t ld, int tid) {
+// 64 x 64 row-major tile (ld) <-> 128 threads x 2 rows of 16-byte pieces: thread t of RP_RW*256
+// holds pieces p = t + RP_RW*256 h, h < 4/RP_RW (row p / 16, columns 4 (p % 16) .. +3)
+#define RP_PPT (4 / RP_RW)
+__device__ __forceinline__ void rp_load(f4_t (&pc)[RP_PPT], const float* T, int64_t ld, int tid) {
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int p = tid + 256 * h;
+    for (int h = 0; h < RP_PPT; ++h) {
+        const int p = tid + RP_RW * 256 * h;
         pc[h] = *reinterpret_cast<const f4_t*>(T + (int64_t)(p >> 4) * ld + 4 * (p & 15));
     }
 }
-__device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[4], bool h3, int tid) {
+__device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[RP_PPT], bool h3, int tid) {
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int p = tid + 256 * h, row = p >> 4, col = 4 * (p & 15), sl = col >> 5, c = col & 31;
+    for (int h = 0; h < RP_PPT; ++h) {
+        const int p = tid + RP_RW * 256 * h, row = p >> 4, col = 4 * (p & 15), sl = col >> 5,
+                  c = col & 31;
         if (h3) {
             h4_t hi, lo;
             split_h3(pc[h], hi, lo);
@@ -737,70 +742,132 @@ __device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[4], bool h3, 
     }
 }
 
+// the workgroup's operand sequence from panel column k0: per column kk, inv(L_kk) (jj == kk),
+// then L_jj,kk for jj = kk+1 .. nc-1; step s -> (kk, jj), false past the end
+__device__ __forceinline__ bool rp_seq(int s, int k0, int nc, int& kk, int& jj) {
+    kk = k0;
+    while (kk < nc && s >= nc - kk) {
+        s -= nc - kk;
+        ++kk;
+    }
+    jj = kk + s;
+    return kk < nc;
+}
+
 template <bool H3>
-__global__ __launch_bounds__(256, 2) void k_panel_rows32(MatF A, int K, int ncols, int row0, int R,
-                                                         int zrow, int nchains,
-                                                         const float* __restrict__ Dinv,
-                                                         int64_t dstride, Live live, int hlim,
-                                                         const int* __restrict__ h3ok) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
-    // XCD-aware, chain-major (as the walk's BULK mapping): one chain's rows share an L2
-    const long rows = R - row0, total = rows * nchains, L = blockIdx.x;
-    const long xcd = L & 7, q = total >> 3, rm = total & 7;
+__global__ __launch_bounds__(256 * RP_RW, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_panel_rows32(MatF A, int K, int ncols, int row0,
+                                                                 int R, int zrow, int nchains,
+                                                                 const float* __restrict__ Dinv,
+                                                                 int64_t dstride, Live live,
+                                                                 int hlim,
+                                                                 const int* __restrict__ h3ok) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = wv >> 2, lw = wv & 3;
+    const int wr = lw >> 1, wc = lw & 1;
+    // XCD-aware, chain-major: one chain's row groups share an L2
+    const long rows = R - row0, ngrp = (rows + RP_RW - 1) / RP_RW, total = ngrp * nchains;
+    const long L = blockIdx.x, xcd = L & 7, q = total >> 3, rm = total & 7;
     const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
-    const int b = (int)(item / rows), i = row0 + (int)(item % rows);
+    const int b = (int)(item / ngrp), i0 = row0 + (int)(item % ngrp) * RP_RW;
     if (!live32(live, b)) return;
-    // fp16x3 operands in the updates of rows below hlim of the chains h3ok allows; the two kinds
-    // of rows are two launches of this kernel (H3 a template parameter: one code path each)
-    if ((i < hlim && (!h3ok || h3ok[b])) != H3) return;
-    const int kst = zrow > 0 ? max(0, zrow - 1 - i - K) : 0;  // first nonzero panel column
-    if (kst >= ncols) return;
+    // row i0 + g of this group: valid, of this launch's operand kind (fp16x3 below hlim in the
+    // chains h3ok allows; the other rows are the other launch's), first nonzero panel column
+    __shared__ int kmin_s;
+    const int i = i0 + g;
+    const bool h3row = i < hlim && (!h3ok || h3ok[b]);
+    const int kst = (zrow > 0 && 2 * i >= zrow) ? max(0, zrow - 1 - i - K) : 0;
+    const bool mine = i < R && h3row == H3 && kst < ncols;
+    if (tid == 0) kmin_s = ncols;
+    __syncthreads();
+    if (mine && lw == 0 && lane == 0) atomicMin(&kmin_s, kst);
+    __syncthreads();
+    const int k0 = kmin_s;  // the workgroup's first column (uniform)
+    if (k0 >= ncols) return;
     __shared__ RowPanelSmem sm;
     float* Ab = A.base + b * A.cstride;
-    float* Ai = Ab + (int64_t)(i * 64) * A.ld;
+    float* Ai = Ab + (int64_t)((mine ? i : i0) * 64) * A.ld;
     const float* Db = Dinv + b * dstride;
-    // the row's panel tiles, register resident: every index below is a compile-time constant
-    // (fully unrolled loops with uniform run-time guards), so nothing goes to scratch
+    auto op_ptr = [&](int s, const float*& p, int64_t& ld, bool& d) -> bool {
+        int kk, jj;
+        if (!rp_seq(s, k0, ncols, kk, jj)) return false;
+        d = jj == kk;
+        p = d ? Db + (int64_t)(K + kk) * 4096 : Ab + (int64_t)((K + jj) * 64) * A.ld + (K + kk) * 64;
+        ld = d ? 64 : A.ld;
+        return true;
+    };
+    // update sums U_ij of the row's panel tiles, register resident: every index below is a
+    // compile-time constant (unrolled loops, uniform run-time guards), so nothing goes to scratch
     f4_t acc[RP_NC][2][2];
 #pragma unroll
     for (int kk = 0; kk < RP_NC; ++kk)
-        if (kk >= kst && kk < ncols) tile32_load(acc[kk], Ai + (K + kk) * 64, A.ld, wr, wc, lane);
-    f4_t pre[4];
-    rp_load(pre, Db + (int64_t)(K + kst) * 4096, 64, tid);  // inv(L_kk) of the first column
-#pragma unroll
-    for (int kk = 0; kk < RP_NC; ++kk) {
-        if (kk < kst || kk >= ncols) continue;
-        const int k = K + kk;
-        // TRSM x = A_ik inv(L_kk)^T on f32 MFMA (k_chol_panel32's product)
-        rp_stage_acc(sm.a, acc[kk], 1.0f, false, wr, wc, lane);
-        rp_stage(sm.b[0], pre, false, tid);
-        __syncthreads();
-        if (kk + 1 < ncols) rp_load(pre, Ab + (int64_t)((K + kk + 1) * 64) * A.ld + k * 64, A.ld, tid);
-        f4_t x[2][2];
 #pragma unroll
         for (int x0 = 0; x0 < 2; ++x0)
 #pragma unroll
-            for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
-        rp_gemm(x, sm.a, sm.b[0], false, wr, wc, lane);
-        tile32_store(x, Ai + k * 64, A.ld, wr, wc, lane);
+            for (int y0 = 0; y0 < 2; ++y0) acc[kk][x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
+    // operands s, s+1 in flight (register sets pe / po by the parity of s: named, so that they
+    // stay in registers), s staged in b[s & 1]
+    f4_t pe[RP_PPT], po[RP_PPT];
+    const float* p0;
+    int64_t ld0;
+    bool d0;
+    op_ptr(0, p0, ld0, d0);
+    rp_load(pe, p0, ld0, tid);
+    if (op_ptr(1, p0, ld0, d0)) rp_load(po, p0, ld0, tid);
+    rp_stage(sm.b[0], pe, false, tid);  // step 0 is inv(L_k0k0)
+    int s = 0;
+    // step s done: load operand s+2 into the set of s, stage operand s+1 into b[(s+1) & 1]
+    auto advance = [&]() {
+        const float* pn;
+        int64_t ldn;
+        bool dn;
+        const bool even = (s & 1) == 0;
+        if (op_ptr(s + 2, pn, ldn, dn)) {
+            if (even) rp_load(pe, pn, ldn, tid);
+            else rp_load(po, pn, ldn, tid);
+        }
+        if (op_ptr(s + 1, pn, ldn, dn)) {
+            if (even) rp_stage(sm.b[1], po, H3 && !dn, tid);
+            else rp_stage(sm.b[0], pe, H3 && !dn, tid);
+        }
+    };
+#pragma unroll
+    for (int kk = 0; kk < RP_NC; ++kk) {
+        if (kk >= k0 && kk < ncols) {
+        const int k = K + kk;
+        const bool act = mine && kk >= kst;
+        // TRSM x = (U_ik + A_ik) inv(L_kk)^T on f32 MFMA (k_chol_panel32's product)
+        f4_t x[2][2];
+        if (act) {
+            tile32_load(x, Ai + k * 64, A.ld, wr, wc, lane);  // the old tile, added last
+#pragma unroll
+            for (int x0 = 0; x0 < 2; ++x0)
+#pragma unroll
+                for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = acc[kk][x0][y0] + x[x0][y0];
+            rp_stage_acc(sm.a[g], x, 1.0f, false, wr, wc, lane);
+        }
         __syncthreads();
-        if (kk + 1 >= ncols) break;
-        // updates of the row's later tiles: acc_j -= x L_jk^T
-        rp_stage_acc(sm.a, x, -1.0f, H3, wr, wc, lane);
-        rp_stage(sm.b[0], pre, H3, tid);
+        if (act) {
+#pragma unroll
+            for (int x0 = 0; x0 < 2; ++x0)
+#pragma unroll
+                for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
+            rp_gemm(x, sm.a[g], sm.b[s & 1], false, wr, wc, lane);
+            tile32_store(x, Ai + k * 64, A.ld, wr, wc, lane);
+        }
+        __syncthreads();  // a[g] and b[s & 1] free
+        advance();
+        if (act && kk + 1 < ncols) rp_stage_acc(sm.a[g], x, -1.0f, H3, wr, wc, lane);
         __syncthreads();
+        ++s;
+        // updates of the row's later tiles: U_ij -= x L_jk^T
 #pragma unroll
         for (int jj = kk + 1; jj < RP_NC; ++jj) {
-            if (jj >= ncols) break;
-            const int cur = (jj - kk - 1) & 1;
-            // next operand in flight: L_(j+1)k, or inv(L_(k+1)(k+1)) after the last update
-            if (jj + 1 < ncols)
-                rp_load(pre, Ab + (int64_t)((K + jj + 1) * 64) * A.ld + k * 64, A.ld, tid);
-            else
-                rp_load(pre, Db + (int64_t)(k + 1) * 4096, 64, tid);
-            rp_gemm(acc[jj], sm.a, sm.b[cur], H3, wr, wc, lane);
-            if (jj + 1 < ncols) rp_stage(sm.b[cur ^ 1], pre, H3, tid);
-            __syncthreads();
+            if (jj < ncols) {
+                if (act) rp_gemm(acc[jj], sm.a[g], sm.b[s & 1], H3, wr, wc, lane);
+                advance();
+                __syncthreads();
+                ++s;
+            }
+        }
         }
     }
 }
@@ -809,12 +876,13 @@ void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, co
                          int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
                          hipStream_t s) {
     if (ncols < 1 || R <= row0) return;
-    const dim3 grid((unsigned)((long)(R - row0) * nchains));
+    const long ngrp = (R - row0 + RP_RW - 1) / RP_RW;
+    const dim3 grid((unsigned)(ngrp * nchains));
     if (hlim > row0)
-        hipLaunchKernelGGL(k_panel_rows32<true>, grid, dim3(256), 0, s, A, K, ncols, row0, R, zrow,
-                           nchains, Dinv, dstride, live, hlim, h3ok);
-    hipLaunchKernelGGL(k_panel_rows32<false>, grid, dim3(256), 0, s, A, K, ncols, row0, R, zrow,
-                       nchains, Dinv, dstride, live, hlim, h3ok);
+        hipLaunchKernelGGL(k_panel_rows32<true>, grid, dim3(256 * RP_RW), 0, s, A, K, ncols, row0,
+                           R, zrow, nchains, Dinv, dstride, live, hlim, h3ok);
+    hipLaunchKernelGGL(k_panel_rows32<false>, grid, dim3(256 * RP_RW), 0, s, A, K, ncols, row0, R,
+                       zrow, nchains, Dinv, dstride, live, hlim, h3ok);
 }
 
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
