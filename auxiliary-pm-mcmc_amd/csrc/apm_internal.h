@@ -17,9 +17,6 @@ struct MatF {
     int64_t cstride;
 };
 
-// widest outer panel the row-panel TRSM kernels (k_panel_rows32 / k_panel_rows64) take
-#define RP_NCOLS 8
-
 // Per-chain liveness: a kernel does work for chain b iff active[b] != 0 && status[b] == 0.
 struct Live {
     const int* active;
@@ -38,11 +35,6 @@ void launch_chol_diag(MatB A, int k, double* Dinv, int64_t dstride, double* ldet
 // panel rows [i0, R) minus the row tiles [glo, ghi) (pass glo = ghi = R for none)
 void launch_chol_panel(MatB A, int k, int i0, int R, int glo, int ghi, const double* Dinv,
                        int64_t dstride, Live live, int nchains, hipStream_t s);
-// rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is factored (Dinv: its
-// tiles' inverses), solved right-looking with each row's panel tiles in registers (chol.hip
-// k_panel_rows64; ncols <= RP_NCOLS); zrow > 0: row tile i is zero before column zrow - 1 - i
-void launch_panel_rows64(MatB A, int K, int ncols, int row0, int R, int zrow, const double* Dinv,
-                         int64_t dstride, Live live, int nchains, hipStream_t s);
 // Optional diag step fused into an update launch (the launch's tiles[0] is the diagonal tile
 // (d, d); Dinv / ldet / status are written as by launch_chol_diag for k = d).
 template <class TS>
@@ -98,11 +90,6 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
                               FusedDiag<float> fd, Live live, int nchains, int hlim,
                               const int* h3ok, hipStream_t s);
-// the same rows solved right-looking with each row's panel tiles in registers (chol32.hip
-// k_panel_rows32): ncols <= RP_NCOLS; Dinv / dstride: the diagonal tiles' fp32 inverses
-void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, const float* Dinv,
-                         int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
-                         hipStream_t s);
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},

@@ -38,7 +38,7 @@ struct apm_ctx {
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
     // tiles per outer panel of the fp64 factorisations (APM_OUTER) and of the Newton matrix
     // (<= 14: the dataflow panel's progress word packs the column step in 4 bits, 15 = failed;
-    // rhs_row_update32 covers a depth of 16 tiles; <= RP_NCOLS for the row-panel kernels)
+    // rhs_row_update32 covers a depth of 16 tiles)
     int outer = 8, outer32 = 8;
     std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
     std::vector<int> slot_wide;  // host mirror of Sl.wide (read back with each theta-call)
@@ -104,10 +104,6 @@ struct apm_ctx {
     // in-panel factorisation of the Newton matrix: one dataflow launch per outer panel
     // (k_chol_panel_df32; APM_DF32=0: the launch sequence it replaces)
     bool df32 = true;
-    // the rows below each outer panel's diagonal block by the row-panel TRSM kernels
-    // (k_panel_rows32 / k_panel_rows64), in every factorisation; APM_ROWPANEL=0: those rows are
-    // part of the dataflow walk (Newton) or of the per-column launches (fp64)
-    bool rowpanel = true;
     unsigned long long* dfprog = nullptr;  // per (chain, row tile) progress words
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
@@ -312,31 +308,18 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
         if (fuse) {
             // left-looking inside the outer panel: column k receives all of the panel's earlier
             // columns in ONE update (depth (k-K)*64, one read-modify-write of its tiles instead
-            // of k-K), whose first tile is the diagonal tile it then factors (fused diag). With
-            // the row-panel kernel these launches cover the diagonal block's rows only, and the
-            // rows below it are solved in one launch once the block is factored.
-            const bool rp = c->rowpanel && Kend - K <= RP_NCOLS && R > Kend;
-            const int Rp = rp ? Kend : R;
+            // of k-K), whose first tile is the diagonal tile it then factors (fused diag)
             for (int k = K; k < Kend; ++k) {
                 const Gap g = gap(k, c->nb);
                 if (k > K)
-                    tracked_update(c, M, K, k - K, k, Rp, k, k + 1, g, false, count, k, fail_code,
-                                   &E);
+                    tracked_update(c, M, K, k - K, k, R, k, k + 1, g, false, count, k, fail_code, &E);
                 else if (!have_diag) {
                     launch_chol_diag(M, k, E.Dinv, c->dstride, E.ldet, c->lstride, lv,
                                      fail_code, count, E.s);
                     check_launch();
                 }
-                launch_chol_panel(M, k, k + 1, Rp, g.lo, g.hi, E.Dinv, c->dstride, lv, count,
+                launch_chol_panel(M, k, k + 1, R, g.lo, g.hi, E.Dinv, c->dstride, lv, count,
                                   E.s);
-                check_launch();
-            }
-            if (rp) {
-                // zero pattern of the stacked posterior factorisation (y_gap: row tile nb + I
-                // zero before tile column nb - 1 - I)
-                const int zrow = gap == y_gap ? 2 * c->nb : 0;
-                launch_panel_rows64(M, K, Kend - K, Kend, R, zrow, E.Dinv, c->dstride, lv, count,
-                                    E.s);
                 check_launch();
             }
             if (after_panel) after_panel(K, Kend);
@@ -427,8 +410,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
-            const bool rp = c->rowpanel && Kend - K <= RP_NCOLS;
-            if (!launch_chol_panel_df32(M, K, Kend - K, rp ? std::min(R, Kend) : R,
+            if (!launch_chol_panel_df32(M, K, Kend - K, R,
                                         FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code},
                                         lv, count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog,
                                         c->nb + 1,
@@ -436,11 +418,6 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                         c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream))
                 throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
-            if (rp) {  // the rows below the diagonal block, once it is factored
-                launch_panel_rows32(M, K, Kend - K, Kend, R, 0, D, ds, lv, count,
-                                    c->h3_now ? c->nb : 0, c->h3ok, c->stream);
-                check_launch();
-            }
             have_diag = Kend < k1;
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                              fail_code);
@@ -806,13 +783,9 @@ void post_bottom32_steps(apm_ctx* c, int count, int K, int Kend, hipStream_t s) 
     const int64_t ds32 = 2 * c->dstride;
     const int hlim = c->h3 ? 2 * nb : 0;
     const int row0 = std::max(nb, 2 * nb - Kend);  // rows with a nonzero tile in the panel
-    if (c->rowpanel && Kend - K <= RP_NCOLS)
-        launch_panel_rows32(S, K, Kend - K, row0, 2 * nb, 2 * nb, d32post_of(c), ds32, lv, count,
-                            hlim, c->h3post, s);
-    else
-        launch_chol_panel_bulk32(S, K, Kend - K, row0, 2 * nb, 2 * nb,
-                                 FusedDiag<float>{0, d32post_of(c), ds32, nullptr, 0, 0}, lv,
-                                 count, hlim, c->h3post, s);
+    launch_chol_panel_bulk32(S, K, Kend - K, row0, 2 * nb, 2 * nb,
+                             FusedDiag<float>{0, d32post_of(c), ds32, nullptr, 0, 0}, lv, count,
+                             hlim, c->h3post, s);
     check_launch();
     if (Kend >= nb) return;
     const auto sl = super_list(c, row0, 2 * nb, Kend, nb, Gap{0, 0});
@@ -1066,7 +1039,6 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
-    if (const char* e = getenv("APM_ROWPANEL")) c->rowpanel = atoi(e) != 0;
     if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;

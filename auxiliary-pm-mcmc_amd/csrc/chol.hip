@@ -174,170 +174,6 @@ __device__ __forceinline__ bool chain_live(const Live& lv, int b) {
 // Stand-alone diag step (one wave per chain): tile (k, k) -> LDS, diag_compute + diag_store (diag.h). Used for
 // the first column of every factorisation; every later diagonal tile is factored inside the
 // update launch that produces it (k_chol_update below, fuse_diag).
-// ----------------------------------------------------------- row-panel TRSM of the bulk rows (fp64)
-// The fp64 twin of chol32.hip's k_panel_rows32: rows [row0, R) below an outer panel whose
-// diagonal block L11 is factored get L_i,P = A_i,P L11^-T over the panel's tile columns
-// P = [K, K + ncols) (ncols <= RP_NCOLS) in one launch, right-looking inside the workgroup with the
-// row's panel update sums in registers (8 waves, wave w owns 16 x 32 of every tile: 2 accumulators
-// of v_mfma_f64_16x16x4_f64 per tile), instead of the per-column launch pairs (left-looking
-// update, then panel TRSM), whose updates re-read the row's earlier panel tiles. Per column k:
-// x = (U_ik + A_ik) inv(L_kk)^T (stored, staged in LDS negated), then every later tile's sum
-// U_ij receives -x L_jk^T; the B operands (inv(L_kk), L_jk) stream through LDS with two operands
-// of loads in flight. The products accumulate in the launch sequence's order (k_chol_update sums
-// its slices from zero and adds the old tile last; k_chol_panel's product), so the factor is
-// bitwise the launch sequence's. zrow > 0: row tile i >= zrow / 2 is zero before tile column
-// zrow - 1 - i (the stacked posterior factorisation's L_K J).
-#define RP64_NC RP_NCOLS
-#define RPP 65  // LDS pitch (doubles)
-struct RowPanelSmem64 {
-    double a[64][RPP];
-    double b[2][64][RPP];
-};
-
-__device__ __forceinline__ void rp64_gemm(d4_t (&acc)[2], const double (*A)[RPP], const double (*B)[RPP],
-                                          int br, int bc0, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        const double a = A[16 * br + r16][4 * t + kq];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, B[16 * (bc0 + j) + r16][4 * t + kq],
-                                                          acc[j], 0, 0, 0);
-    }
-}
-__device__ __forceinline__ void rp64_stage_acc(double (*A)[RPP], const d4_t (&v)[2], double sgn,
-                                               int br, int bc0, int lane) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            A[16 * br + F64_CROW(lane, r)][16 * (bc0 + j) + (lane & 15)] = sgn * v[j][r];
-}
-__device__ __forceinline__ void rp64_load(d2_t (&pc)[4], const double* T, int64_t ld, int tid) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int p = tid + 512 * h;
-        pc[h] = *reinterpret_cast<const d2_t*>(T + (int64_t)(p >> 5) * ld + 2 * (p & 31));
-    }
-}
-__device__ __forceinline__ void rp64_stage(double (*B)[RPP], const d2_t (&pc)[4], int tid) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const int p = tid + 512 * h, row = p >> 5, col = 2 * (p & 31);
-        B[row][col] = pc[h].x;
-        B[row][col + 1] = pc[h].y;
-    }
-}
-// operand sequence from panel column k0: per column kk, inv(L_kk), then L_jj,kk (jj > kk)
-__device__ __forceinline__ bool rp64_seq(int s, int k0, int nc, int& kk, int& jj) {
-    kk = k0;
-    while (kk < nc && s >= nc - kk) {
-        s -= nc - kk;
-        ++kk;
-    }
-    jj = kk + s;
-    return kk < nc;
-}
-
-__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_panel_rows64(
-    MatB A, int K, int ncols, int row0, int R, int zrow, int nchains, const double* __restrict__ Dinv,
-    int64_t dstride, Live live) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, br = wv >> 1, bc0 = 2 * (wv & 1);
-    const long rows = R - row0, total = rows * nchains, L = blockIdx.x;
-    const long xcd = L & 7, q = total >> 3, rm = total & 7;
-    const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
-    const int b = (int)(item / rows), i = row0 + (int)(item % rows);
-    if (!chain_live(live, b)) return;
-    const int k0 = (zrow > 0 && 2 * i >= zrow) ? max(0, zrow - 1 - i - K) : 0;
-    if (k0 >= ncols) return;
-    __shared__ RowPanelSmem64 sm;
-    double* Ab = A.base + b * A.cstride;
-    double* Ai = Ab + (int64_t)(i * 64) * A.ld;
-    const double* Db = Dinv + b * dstride;
-    auto op_ptr = [&](int s, const double*& p, int64_t& ld) -> bool {
-        int kk, jj;
-        if (!rp64_seq(s, k0, ncols, kk, jj)) return false;
-        p = jj == kk ? Db + (int64_t)(K + kk) * 4096 : Ab + (int64_t)((K + jj) * 64) * A.ld + (K + kk) * 64;
-        ld = jj == kk ? 64 : A.ld;
-        return true;
-    };
-    auto tload = [&](d4_t (&v)[2], const double* T) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                v[j][r] = T[(int64_t)(16 * br + F64_CROW(lane, r)) * A.ld + 16 * (bc0 + j) + (lane & 15)];
-    };
-    auto tstore = [&](const d4_t (&v)[2], double* T) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                T[(int64_t)(16 * br + F64_CROW(lane, r)) * A.ld + 16 * (bc0 + j) + (lane & 15)] = v[j][r];
-    };
-    d4_t acc[RP64_NC][2];  // update sums, register resident (compile-time indices only)
-#pragma unroll
-    for (int kk = 0; kk < RP64_NC; ++kk) acc[kk][0] = acc[kk][1] = d4_t{0.0, 0.0, 0.0, 0.0};
-    d2_t pe[4], po[4];  // operands s, s+1 in flight by the parity of s
-    const double* p0;
-    int64_t ld0;
-    op_ptr(0, p0, ld0);
-    rp64_load(pe, p0, ld0, tid);
-    if (op_ptr(1, p0, ld0)) rp64_load(po, p0, ld0, tid);
-    rp64_stage(sm.b[0], pe, tid);
-    int s = 0;
-    auto advance = [&]() {  // load operand s+2 into the set of s, stage s+1 into b[(s+1) & 1]
-        const double* pn;
-        int64_t ldn;
-        const bool even = (s & 1) == 0;
-        if (op_ptr(s + 2, pn, ldn)) {
-            if (even) rp64_load(pe, pn, ldn, tid);
-            else rp64_load(po, pn, ldn, tid);
-        }
-        if (op_ptr(s + 1, pn, ldn)) {
-            if (even) rp64_stage(sm.b[1], po, tid);
-            else rp64_stage(sm.b[0], pe, tid);
-        }
-    };
-#pragma unroll
-    for (int kk = 0; kk < RP64_NC; ++kk) {
-        if (kk >= k0 && kk < ncols) {
-            const int k = K + kk;
-            d4_t x[2];
-            tload(x, Ai + k * 64);  // the old tile, added after the update sum
-            x[0] = acc[kk][0] + x[0];
-            x[1] = acc[kk][1] + x[1];
-            rp64_stage_acc(sm.a, x, 1.0, br, bc0, lane);  // TRSM x = (U + A_ik) inv(L_kk)^T
-            __syncthreads();
-            x[0] = x[1] = d4_t{0.0, 0.0, 0.0, 0.0};
-            rp64_gemm(x, sm.a, sm.b[s & 1], br, bc0, lane);
-            tstore(x, Ai + k * 64);
-            __syncthreads();
-            advance();
-            if (kk + 1 < ncols) rp64_stage_acc(sm.a, x, -1.0, br, bc0, lane);  // -L_ik
-            __syncthreads();
-            ++s;
-#pragma unroll
-            for (int jj = kk + 1; jj < RP64_NC; ++jj) {
-                if (jj < ncols) {
-                    rp64_gemm(acc[jj], sm.a, sm.b[s & 1], br, bc0, lane);
-                    advance();
-                    __syncthreads();
-                    ++s;
-                }
-            }
-        }
-    }
-}
-
-void launch_panel_rows64(MatB A, int K, int ncols, int row0, int R, int zrow, const double* Dinv,
-                         int64_t dstride, Live live, int nchains, hipStream_t s) {
-    if (ncols < 1 || R <= row0) return;
-    hipLaunchKernelGGL(k_panel_rows64, dim3((unsigned)((long)(R - row0) * nchains)), dim3(512), 0,
-                       s, A, K, ncols, row0, R, zrow, nchains, Dinv, dstride, live);
-}
-
 template <class Mat, class TS>
 __global__ __launch_bounds__(64) void k_chol_diag(Mat A, int k, TS* Dinv, int64_t dstride,
                                                   double* ldet, int64_t lstride, Live live,

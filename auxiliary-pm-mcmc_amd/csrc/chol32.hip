@@ -622,269 +622,6 @@ bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
     return true;
 }
 
-// ----------------------------------------------------------- row-panel TRSM of the bulk rows
-// Rows below an outer panel whose diagonal block L11 is factored (tiles and their inverses final):
-// L_i,P = A_i,P L11^-T over the panel's tile columns P = [K, K + ncols), ncols <= RP_NC. The
-// dataflow walk (k_chol_panel_df32) solves a row left-looking and re-reads the row's earlier panel
-// tiles from memory at each of its ncols dependent column steps (~95 us per walk).
-// Here a workgroup of RP_RW x 4 waves takes RP_RW rows of one chain; each row's panel tiles stay
-// in registers (wave (wr, wc) of the row's group holds its 32 x 32 quadrant of every tile) and the
-// row is solved right-looking: per column k, the TRSM x = (U_ik + A_ik) inv(L_kk)^T (f32 MFMA) is
-// stored and staged once in LDS (negated; hi/lo for fp16x3 rows), and every later tile's update sum
-// U_ij receives -x L_jk^T. The B operands - inv(L_kk) and the tiles L_jk of the diagonal block -
-// are the same for every row of the chain: they stream through LDS once per workgroup (shared by
-// its rows), two operands of global loads in flight ahead of the one multiplied. Accumulation is
-// in the walk's order (each U_ij sums its products from zero in column order, the old tile A_ij
-// is added before the TRSM, as tile_gemm_nt32 adds C after its products), so the factor is
-// bitwise the walk's.
-#define RP_NC RP_NCOLS
-#define RP_RW 2  // rows per workgroup
-union RPOp {
-    float f[2][64][LP32];
-    struct {
-        _Float16 h[2][64][LPH], l[2][64][LPH];
-    } x;
-};
-struct RowPanelSmem {
-    RPOp a[RP_RW];  // per row: the A operand, A_ik (TRSM) or -L_ik (updates)
-    RPOp b[2];      // the shared B operand, inv(L_kk) (TRSM) or L_jk (updates), double-buffered
-};
-
-// acc += A B^T over one 64-deep operand pair (two 32-deep slices), the MFMA sequence of
-// tile_gemm_nt32 (fp16x3: hi.hi, hi.lo, lo.hi per 16x16x32 block)
-__device__ __forceinline__ void rp_gemm(f4_t (&acc)[2][2], const RPOp& A, const RPOp& B, bool h3,
-                                        int wr, int wc, int lane) {
-    const int r16 = lane & 15, kq = lane >> 4;
-    if (h3) {
-#pragma unroll
-        for (int cur = 0; cur < 2; ++cur) {
-            h8_t ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-            for (int x = 0; x < 2; ++x) {
-                ah[x] = *reinterpret_cast<const h8_t*>(&A.x.h[cur][32 * wr + 16 * x + r16][8 * kq]);
-                al[x] = *reinterpret_cast<const h8_t*>(&A.x.l[cur][32 * wr + 16 * x + r16][8 * kq]);
-                bh[x] = *reinterpret_cast<const h8_t*>(&B.x.h[cur][32 * wc + 16 * x + r16][8 * kq]);
-                bl[x] = *reinterpret_cast<const h8_t*>(&B.x.l[cur][32 * wc + 16 * x + r16][8 * kq]);
-            }
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj) {
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-                }
-        }
-        return;
-    }
-#pragma unroll
-    for (int cur = 0; cur < 2; ++cur)
-#pragma unroll
-        for (int t = 0; t < KS32 / 4; ++t) {
-            float a[2], bb[2];
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi) a[bi] = A.f[cur][32 * wr + 16 * bi + r16][4 * t + kq];
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj) bb[bj] = B.f[cur][32 * wc + 16 * bj + r16][4 * t + kq];
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj)
-                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj], acc[bi][bj], 0, 0, 0);
-        }
-}
-
-// a wave's 32 x 32 quadrant (times sgn) -> operand slice wc (rows 32 wr ..); fp32, or fp16 hi / lo
-__device__ __forceinline__ void rp_stage_acc(RPOp& O, const f4_t (&v)[2][2], float sgn, bool h3,
-                                             int wr, int wc, int lane) {
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 32 * wr + 16 * bi + F32_CROW(lane, r), col = 16 * bj + (lane & 15);
-                const float x = sgn * v[bi][bj][r];
-                if (h3) {
-                    const _Float16 hx = (_Float16)x;
-                    O.x.h[wc][row][col] = hx;
-                    O.x.l[wc][row][col] = (_Float16)(x - (float)hx);
-                } else {
-                    O.f[wc][row][col] = x;
-                }
-            }
-}
-
-// 64 x 64 row-major tile (ld) <-> 128 threads x 2 rows of 16-byte pieces: thread t of RP_RW*256
-// holds pieces p = t + RP_RW*256 h, h < 4/RP_RW (row p / 16, columns 4 (p % 16) .. +3)
-#define RP_PPT (4 / RP_RW)
-__device__ __forceinline__ void rp_load(f4_t (&pc)[RP_PPT], const float* T, int64_t ld, int tid) {
-#pragma unroll
-    for (int h = 0; h < RP_PPT; ++h) {
-        const int p = tid + RP_RW * 256 * h;
-        pc[h] = *reinterpret_cast<const f4_t*>(T + (int64_t)(p >> 4) * ld + 4 * (p & 15));
-    }
-}
-__device__ __forceinline__ void rp_stage(RPOp& O, const f4_t (&pc)[RP_PPT], bool h3, int tid) {
-#pragma unroll
-    for (int h = 0; h < RP_PPT; ++h) {
-        const int p = tid + RP_RW * 256 * h, row = p >> 4, col = 4 * (p & 15), sl = col >> 5,
-                  c = col & 31;
-        if (h3) {
-            h4_t hi, lo;
-            split_h3(pc[h], hi, lo);
-            *reinterpret_cast<h4_t*>(&O.x.h[sl][row][c]) = hi;
-            *reinterpret_cast<h4_t*>(&O.x.l[sl][row][c]) = lo;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) O.f[sl][row][c + e] = pc[h][e];
-        }
-    }
-}
-
-// the workgroup's operand sequence from panel column k0: per column kk, inv(L_kk) (jj == kk),
-// then L_jj,kk for jj = kk+1 .. nc-1; step s -> (kk, jj), false past the end
-__device__ __forceinline__ bool rp_seq(int s, int k0, int nc, int& kk, int& jj) {
-    kk = k0;
-    while (kk < nc && s >= nc - kk) {
-        s -= nc - kk;
-        ++kk;
-    }
-    jj = kk + s;
-    return kk < nc;
-}
-
-template <bool H3>
-__global__ __launch_bounds__(256 * RP_RW, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_panel_rows32(MatF A, int K, int ncols, int row0,
-                                                                 int R, int zrow, int nchains,
-                                                                 const float* __restrict__ Dinv,
-                                                                 int64_t dstride, Live live,
-                                                                 int hlim,
-                                                                 const int* __restrict__ h3ok) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = wv >> 2, lw = wv & 3;
-    const int wr = lw >> 1, wc = lw & 1;
-    // XCD-aware, chain-major: one chain's row groups share an L2
-    const long rows = R - row0, ngrp = (rows + RP_RW - 1) / RP_RW, total = ngrp * nchains;
-    const long L = blockIdx.x, xcd = L & 7, q = total >> 3, rm = total & 7;
-    const long item = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (L >> 3);
-    const int b = (int)(item / ngrp), i0 = row0 + (int)(item % ngrp) * RP_RW;
-    if (!live32(live, b)) return;
-    // row i0 + g of this group: valid, of this launch's operand kind (fp16x3 below hlim in the
-    // chains h3ok allows; the other rows are the other launch's), first nonzero panel column
-    __shared__ int kmin_s;
-    const int i = i0 + g;
-    const bool h3row = i < hlim && (!h3ok || h3ok[b]);
-    const int kst = (zrow > 0 && 2 * i >= zrow) ? max(0, zrow - 1 - i - K) : 0;
-    const bool mine = i < R && h3row == H3 && kst < ncols;
-    if (tid == 0) kmin_s = ncols;
-    __syncthreads();
-    if (mine && lw == 0 && lane == 0) atomicMin(&kmin_s, kst);
-    __syncthreads();
-    const int k0 = kmin_s;  // the workgroup's first column (uniform)
-    if (k0 >= ncols) return;
-    __shared__ RowPanelSmem sm;
-    float* Ab = A.base + b * A.cstride;
-    float* Ai = Ab + (int64_t)((mine ? i : i0) * 64) * A.ld;
-    const float* Db = Dinv + b * dstride;
-    auto op_ptr = [&](int s, const float*& p, int64_t& ld, bool& d) -> bool {
-        int kk, jj;
-        if (!rp_seq(s, k0, ncols, kk, jj)) return false;
-        d = jj == kk;
-        p = d ? Db + (int64_t)(K + kk) * 4096 : Ab + (int64_t)((K + jj) * 64) * A.ld + (K + kk) * 64;
-        ld = d ? 64 : A.ld;
-        return true;
-    };
-    // update sums U_ij of the row's panel tiles, register resident: every index below is a
-    // compile-time constant (unrolled loops, uniform run-time guards), so nothing goes to scratch
-    f4_t acc[RP_NC][2][2];
-#pragma unroll
-    for (int kk = 0; kk < RP_NC; ++kk)
-#pragma unroll
-        for (int x0 = 0; x0 < 2; ++x0)
-#pragma unroll
-            for (int y0 = 0; y0 < 2; ++y0) acc[kk][x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
-    // operands s, s+1 in flight (register sets pe / po by the parity of s: named, so that they
-    // stay in registers), s staged in b[s & 1]
-    f4_t pe[RP_PPT], po[RP_PPT];
-    const float* p0;
-    int64_t ld0;
-    bool d0;
-    op_ptr(0, p0, ld0, d0);
-    rp_load(pe, p0, ld0, tid);
-    if (op_ptr(1, p0, ld0, d0)) rp_load(po, p0, ld0, tid);
-    rp_stage(sm.b[0], pe, false, tid);  // step 0 is inv(L_k0k0)
-    int s = 0;
-    // step s done: load operand s+2 into the set of s, stage operand s+1 into b[(s+1) & 1]
-    auto advance = [&]() {
-        const float* pn;
-        int64_t ldn;
-        bool dn;
-        const bool even = (s & 1) == 0;
-        if (op_ptr(s + 2, pn, ldn, dn)) {
-            if (even) rp_load(pe, pn, ldn, tid);
-            else rp_load(po, pn, ldn, tid);
-        }
-        if (op_ptr(s + 1, pn, ldn, dn)) {
-            if (even) rp_stage(sm.b[1], po, H3 && !dn, tid);
-            else rp_stage(sm.b[0], pe, H3 && !dn, tid);
-        }
-    };
-#pragma unroll
-    for (int kk = 0; kk < RP_NC; ++kk) {
-        if (kk >= k0 && kk < ncols) {
-        const int k = K + kk;
-        const bool act = mine && kk >= kst;
-        // TRSM x = (U_ik + A_ik) inv(L_kk)^T on f32 MFMA (k_chol_panel32's product)
-        f4_t x[2][2];
-        if (act) {
-            tile32_load(x, Ai + k * 64, A.ld, wr, wc, lane);  // the old tile, added last
-#pragma unroll
-            for (int x0 = 0; x0 < 2; ++x0)
-#pragma unroll
-                for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = acc[kk][x0][y0] + x[x0][y0];
-            rp_stage_acc(sm.a[g], x, 1.0f, false, wr, wc, lane);
-        }
-        __syncthreads();
-        if (act) {
-#pragma unroll
-            for (int x0 = 0; x0 < 2; ++x0)
-#pragma unroll
-                for (int y0 = 0; y0 < 2; ++y0) x[x0][y0] = f4_t{0.f, 0.f, 0.f, 0.f};
-            rp_gemm(x, sm.a[g], sm.b[s & 1], false, wr, wc, lane);
-            tile32_store(x, Ai + k * 64, A.ld, wr, wc, lane);
-        }
-        __syncthreads();  // a[g] and b[s & 1] free
-        advance();
-        if (act && kk + 1 < ncols) rp_stage_acc(sm.a[g], x, -1.0f, H3, wr, wc, lane);
-        __syncthreads();
-        ++s;
-        // updates of the row's later tiles: U_ij -= x L_jk^T
-#pragma unroll
-        for (int jj = kk + 1; jj < RP_NC; ++jj) {
-            if (jj < ncols) {
-                if (act) rp_gemm(acc[jj], sm.a[g], sm.b[s & 1], H3, wr, wc, lane);
-                advance();
-                __syncthreads();
-                ++s;
-            }
-        }
-        }
-    }
-}
-
-void launch_panel_rows32(MatF A, int K, int ncols, int row0, int R, int zrow, const float* Dinv,
-                         int64_t dstride, Live live, int nchains, int hlim, const int* h3ok,
-                         hipStream_t s) {
-    if (ncols < 1 || R <= row0) return;
-    const long ngrp = (R - row0 + RP_RW - 1) / RP_RW;
-    const dim3 grid((unsigned)(ngrp * nchains));
-    if (hlim > row0)
-        hipLaunchKernelGGL(k_panel_rows32<true>, grid, dim3(256 * RP_RW), 0, s, A, K, ncols, row0,
-                           R, zrow, nchains, Dinv, dstride, live, hlim, h3ok);
-    hipLaunchKernelGGL(k_panel_rows32<false>, grid, dim3(256 * RP_RW), 0, s, A, K, ncols, row0, R,
-                       zrow, nchains, Dinv, dstride, live, hlim, h3ok);
-}
-
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
                               FusedDiag<float> fd, Live live, int nchains, int hlim,
                               const int* h3ok, hipStream_t s) {

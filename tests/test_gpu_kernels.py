@@ -388,47 +388,26 @@ def test_posterior_bottom_fp32_matches_fp64(nat, monkeypatch, n):
 
 @pytest.mark.parametrize('n', [560, 1100])
 def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch, n):
-    """The Newton factor's in-panel steps in three forms with the same operands and the same
+    """The Newton factor's in-panel steps in two forms with the same operands and the same
     accumulation order, so modes, estimates, statuses and iteration counts are bitwise equal - also
     for a batch with a chain at an extreme theta (fp32 operands, possibly a failed fp32
     factorisation and its fp64 rerun) next to ordinary ones: the per-column launch sequence
-    (APM_DF32=0 APM_ROWPANEL=0), one dataflow launch per outer panel whose rows walk the panel's
-    columns (k_chol_panel_df32; APM_ROWPANEL=0), and the default: the dataflow chain for the
-    diagonal block, then the rows below it right-looking with their update sums in registers
-    (k_panel_rows32; k_panel_rows64 in the fp64 factorisations of the same call). n = 560: a last
-    outer panel of one column (its TRSM only), n = 1100: three outer panels, the last of two."""
+    (APM_DF32=0) and the default, one dataflow launch per outer panel whose rows walk the panel's
+    columns (k_chol_panel_df32). n = 560: a last outer panel of one column (its TRSM only),
+    n = 1100: three outer panels, the last of two."""
     X, y, thetas, ns = _mixed_case(n=n)
     ext = thetas[0].copy()
     ext[0] = 45.0
     thetas = np.vstack([thetas, ext])
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0, APM_ROWPANEL=0)
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0)
     assert (s0[:3] == 0).all()
-    for env in (dict(APM_ROWPANEL=0), {}):
-        o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, **env)
-        np.testing.assert_array_equal(s1, s0)
-        np.testing.assert_array_equal(n1, n0)
-        for b in range(len(thetas)):
-            if s0[b] == 0:
-                np.testing.assert_array_equal(f1[b], f0[b])
-                assert o1[b] == o0[b], (env, b, o1[b], o0[b])
-
-
-@pytest.mark.parametrize('n', [560, 1100])
-def test_rowpanel_fp64_matches_launch_sequence(nat, monkeypatch, n):
-    """The fp64 factorisations (chol(K), the stacked posterior factor with its zero pattern, the
-    fp64 Newton) with the rows below each diagonal block solved by k_panel_rows64 (default)
-    against the per-column launches (APM_ROWPANEL=0): the same products in the same order, so the
-    all-fp64 Newton path (APM_MIXED=0) with the all-fp64 posterior factor (APM_POST32=0) gives
-    bitwise equal modes and estimates."""
-    X, y, thetas, ns = _mixed_case(n=n)
-    env = dict(APM_MIXED=0, APM_POST32=0)
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_ROWPANEL=0, **env)
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, **env)
-    assert (s0 == 0).all() and (s1 == 0).all()
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    np.testing.assert_array_equal(s1, s0)
     np.testing.assert_array_equal(n1, n0)
     for b in range(len(thetas)):
-        np.testing.assert_array_equal(f1[b], f0[b])
-        assert o1[b] == o0[b], (b, o1[b], o0[b])
+        if s0[b] == 0:
+            np.testing.assert_array_equal(f1[b], f0[b])
+            assert o1[b] == o0[b], (b, o1[b], o0[b])
 
 
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
