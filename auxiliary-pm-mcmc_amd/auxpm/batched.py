@@ -19,6 +19,11 @@ streams and the masked-failure bookkeeping (``_BatchedChains``):
 * ``BatchedPMMHSampler`` — ``PMMHSampler`` (samplers.py:159-262; BASELINE configs[0] protocol,
   Pseudo-Marginal MH.ipynb cells 12-14): one batched theta-call per iteration at the proposals,
   with the Laplace estimator (adaptive phase) or the IS estimator on fresh u (main phase).
+* ``BatchedAPMMetIndPlusRandDirSliceSampler`` / ``BatchedAPMMetIndPlusMHSampler`` —
+  ``APMMetIndPlusRandDirSliceSampler`` (samplers.py:926-1004 over the MI + SS base
+  :588-710) and ``APMMetIndPlusMHSampler`` (:265-418): the same theta updates, with u updated
+  by a Metropolis independence step (mcmc_updates.py:159-303: a fresh u from the device, one
+  batched u-call against the current cache, accept iff U < exp(log f' - log f)).
 
 Per chain the control flow, the cache protocol and the host-RNG draw order are those of the
 reference (one ``numpy.random.RandomState`` per chain for slice heights, angles, offsets,
@@ -40,7 +45,8 @@ from gpdemo import _native
 from gpdemo.utils import log_prior_ard_batch
 
 __all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler', 'BatchedAPMEllSSPlusMHSampler',
-           'BatchedPMMHSampler', 'chain_streams']
+           'BatchedPMMHSampler', 'BatchedAPMMetIndPlusRandDirSliceSampler',
+           'BatchedAPMMetIndPlusMHSampler', 'chain_streams']
 
 _EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC, 'laplace': _native.EST_LAPLACE}
 
@@ -101,6 +107,7 @@ class _BatchedChains(object):
         # accepted elliptical-slice move — u is a deterministic function of these
         self.u_init_ctr = np.zeros(C, dtype=np.uint64)
         self.u_log = [[] for _ in range(C)]
+        self.n_reject_u = np.zeros(C, dtype=np.int64)  # Metropolis independence u-updates
 
     # ------------------------------------------------------------------ helpers
     def log_prior(self, thetas):
@@ -221,6 +228,37 @@ class _BatchedChains(object):
         return float(np.max(np.abs(lf - saved)))
 
     # ------------------------------------------------------------------ updates
+    def _u_update(self, chains=None):
+        """The u half of a transition (E-SS here; the MI twins override it)."""
+        self._ess_u(chains)
+
+    def _mi_u(self, chains=None):
+        """Metropolis independence update of the u of every live chain (or of the given chains)
+        (mcmc_updates.py:284-303 with the prior as proposal, as samplers.py:700-705): u' from the
+        chain's device stream, one batched u-call against the current cache, then per chain
+        accept iff U < exp(log f' - log f) - the reference's draw order. An accepted u' is logged
+        for ``restore`` as the combination 0 u + 1 u' (k_u_combine reproduces it bit for bit)."""
+        live = np.flatnonzero(~self.failed) if chains is None else \
+            np.asarray(chains, dtype=np.int64)[~self.failed[chains]]
+        if live.size == 0:
+            return
+        ctr = self.dev_ctr.copy()
+        self._normals(live, self.ub_prop)
+        t0 = time.perf_counter()
+        out, st = self.ctx.u_eval(self.slot_cur[live], self.ub_prop[live])
+        self.wall['u_call'] += time.perf_counter() - t0
+        self.n_u_calls += live.size
+        lf = np.where(st == 0, out, -np.inf) + self.lp_cur[live]
+        with np.errstate(over='ignore'):
+            p_acc = np.exp(lf - self.log_f[live])
+        for q, c in enumerate(live):
+            if self.prngs[c].uniform() < p_acc[q]:
+                self.ub_u[c], self.ub_prop[c] = self.ub_prop[c], self.ub_u[c]
+                self.log_f[c] = lf[q]
+                self.u_log[c].append((ctr[c], 0.0, 1.0))
+            else:
+                self.n_reject_u[c] += 1
+
     def _ess_u(self, chains=None):
         """Elliptical slice update of the u of every live chain (or of the given chains),
         mcmc_updates.py:372-400; each shrink round is one batched u-call."""
@@ -379,7 +417,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
     def step(self):
         """One lockstep transition (u then theta) of every live chain; returns thetas
         (n_chains, P)."""
-        self._ess_u()
+        self._u_update()
         self._rdss_theta()
         return self.theta.copy()
 
@@ -478,7 +516,7 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
             go = (~self.failed) & (unfinished if not keep_going else True)
             ess = np.flatnonzero(need_u & go)
             if ess.size:
-                self._ess_u(ess)
+                self._u_update(ess)
                 for c in ess:
                     need_u[c] = False
                     if not self.failed[c]:
@@ -567,18 +605,23 @@ class _BatchedMHMixin(object):
         thetas = np.empty((self.n_chains, n_sample, self.P))
         thetas[:, 0] = self.theta
         self.n_reject[:] = 0
+        self.n_reject_u[:] = 0
         for s in range(1, n_sample):
             thetas[:, s] = self.step()
-        return thetas, self.n_reject.copy()
+        return thetas, self._rejections()
+
+    def _rejections(self):
+        return self.n_reject.copy()
 
     def adaptive_run(self, theta_init, batch_size, n_batch, low_acc_thr, upp_acc_thr,
-                     adapt_factor_func):
+                     adapt_factor_func, reject_count_index=None):
         """BaseAdaptiveMHSampler.adaptive_run (samplers.py:14-156) for every chain: each batch
         restarts get_samples from the previous batch's last state (a fresh estimate there, as
         the reference's get_samples does) and each chain's scales are divided / multiplied by
         adapt_factor_func(b, n_batch) when its batch accept rate is below / above the
-        thresholds. Returns (thetas (C, n_batch*batch_size, P), scales (C, n_batch, P),
-        accept_rates (C, n_batch))."""
+        thresholds. Where get_samples returns several rejection counts (MI + MH: u and theta),
+        ``reject_count_index`` picks the one the scales drive (samplers.py:143-144). Returns
+        (thetas (C, n_batch*batch_size, P), scales (C, n_batch, P), accept_rates (C, n_batch))."""
         C = self.n_chains
         thetas = np.empty((C, n_batch * batch_size, self.P))
         scales = np.empty((C, n_batch, self.P))
@@ -587,6 +630,10 @@ class _BatchedMHMixin(object):
         for b in range(n_batch):
             lo, hi = b * batch_size, (b + 1) * batch_size
             thetas[:, lo:hi], n_reject = self.get_samples(batch_size, th0)
+            if isinstance(n_reject, tuple):
+                if reject_count_index is None:
+                    raise ValueError('several rejection counts: pass reject_count_index')
+                n_reject = n_reject[reject_count_index]
             rates[:, b] = 1. - (n_reject * 1. / batch_size)
             th0 = thetas[:, hi - 1].copy()
             factor = adapt_factor_func(b, n_batch)
@@ -627,7 +674,7 @@ class BatchedAPMEllSSPlusMHSampler(_BatchedMHMixin, _BatchedChains):
 
     def step(self):
         """One transition of every live chain (u by E-SS, then theta by MH); returns thetas."""
-        self._ess_u()
+        self._u_update()
         self._mh_theta()
         return self.theta.copy()
 
@@ -674,3 +721,27 @@ class BatchedPMMHSampler(_BatchedMHMixin, _BatchedChains):
             self.ub_u[c], self.ub_prop[c] = self.ub_prop[c], self.ub_u[c]
         self._decide(live, th_p, lf_p, lp_p, accept)
         return self.theta.copy()
+
+
+class BatchedAPMMetIndPlusRandDirSliceSampler(BatchedAPMEllSSPlusRandDirSliceSampler):
+    """Batch of APM MI(u) + RD-SS(theta) chains (reference APMMetIndPlusRandDirSliceSampler,
+    samplers.py:926-1004; get_samples of its base :661-710): ``step()``, ``run`` and
+    ``run_async`` as the E-SS twin, the u half of every transition a Metropolis independence
+    step (one batched u-call). ``n_reject_u`` counts each chain's rejected u proposals (the
+    reference's ``n_reject``)."""
+
+    def _u_update(self, chains=None):
+        self._mi_u(chains)
+
+
+class BatchedAPMMetIndPlusMHSampler(BatchedAPMEllSSPlusMHSampler):
+    """Batch of APM MI(u) + MH(theta) chains (reference APMMetIndPlusMHSampler,
+    samplers.py:265-418). ``get_samples`` returns (thetas, (n_reject_u, n_reject_theta)) per
+    chain like the reference's (n_reject_1, n_reject_2); ``adaptive_run(...,
+    reject_count_index=1)`` adapts on the theta step as samplers.py:143-144."""
+
+    def _u_update(self, chains=None):
+        self._mi_u(chains)
+
+    def _rejections(self):
+        return self.n_reject_u.copy(), self.n_reject.copy()

@@ -122,6 +122,7 @@ void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double
 // the whole solve in one launch over TRM_G workgroups per chain (k_trsv32_mw; NaN-fills `out`
 // first; fp64 r -> out, r kept); needs np <= 8192 (trsv32_mw_ok), else the per-block steps above
 bool trsv32_mw_ok(int np);
+void trsv32_mw_init();  // per device, once the device is current (apm_create)
 void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
                       int fail_code, hipStream_t s);
@@ -184,11 +185,11 @@ struct SlotSet {
     int64_t lstride, vstride;
     // wide slots (trace of the factor's Gram L L^T above APM_WIDE_Q, ugemm.hip): the factor is
     // also kept in fp64 and their u-path runs on f64 MFMA
-    double* L64;        // np x np per wide slot, ld = np (stride l64stride)
+    double* const* L64; // per slot: np x np, ld = np, or null - buffers are attached by the host
+                        // to the slots that become wide (rare), not allocated per slot
     double* rowq;       // np per slot: squared row norms of the factor (k_slot_write_L)
     int* wide;          // 1 per slot
     int* chain_wide;    // 1 per chain of the call (read back with the theta-call's results)
-    int64_t l64stride;
     double wide_q;      // the threshold (APM_WIDE_Q, overridable by the environment variable)
     double post_q;      // trace(C) above which an fp32 bottom block is recomputed in fp64
                         // (APM_POST32_Q; postcov.hip)
@@ -208,6 +209,9 @@ struct SlotSet {
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
                        int nchains, hipStream_t s, MatF S32 = MatF{nullptr, 0, 0});
+// the fp64 factor alone, for the call's wide slots that have a buffer attached (mode 1 or 2)
+void launch_slot_write_L64(MatB A, SlotSet S, const int64_t* slots, int mode, int np, Live live,
+                           int nchains, hipStream_t s);
 
 // ---- postcov.hip ----------------------------------------------------------------------------
 void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,

@@ -42,6 +42,10 @@ struct apm_ctx {
     int outer = 8, outer32 = 8;
     std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
     std::vector<int> slot_wide;  // host mirror of Sl.wide (read back with each theta-call)
+    // fp64 factors of the wide slots: one np x np buffer attached per wide slot (Sl.L64 is the
+    // device copy of l64_h), returned to l64_free when its slot is rewritten narrow
+    std::vector<double*> l64_h, l64_free;
+    double** l64_d = nullptr;
     double eps = 1e-8, tol = 1e-4;
     int64_t max_iters = 1000;
     std::string err;
@@ -848,6 +852,26 @@ void bottom64_rerun(apm_ctx* c, int count, const std::vector<int>& redo) {
     c->n_post64 += (int64_t)redo.size();
 }
 
+// fp64 factor buffers of wide slots (Sl.L64): attached on demand, recycled through l64_free
+void attach_l64(apm_ctx* c, int64_t slot) {
+    if (c->l64_h[slot]) return;
+    if (!c->l64_free.empty()) {
+        c->l64_h[slot] = c->l64_free.back();
+        c->l64_free.pop_back();
+    } else {
+        c->l64_h[slot] = dalloc<double>(c, c->np * c->np);
+    }
+}
+void detach_l64(apm_ctx* c, int64_t slot) {
+    if (!c->l64_h[slot]) return;
+    c->l64_free.push_back(c->l64_h[slot]);
+    c->l64_h[slot] = nullptr;
+}
+void upload_l64(apm_ctx* c) {  // pageable source: the copy has read it when the call returns
+    HIPC(hipMemcpyAsync(c->l64_d, c->l64_h.data(), sizeof(double*) * c->n_slots,
+                        hipMemcpyHostToDevice, c->stream));
+}
+
 // L_K ready in BL (chol_k_into_bl); h = L_K^-1 f_post = L_K^T a because f_post = K a
 void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     const Live lv = live_of(c);
@@ -994,19 +1018,47 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                       RB{c->status, (int)sizeof(int) * count, st_h.data()},
                       RB{c->n_iter, (int)sizeof(int) * count, it_h.data()},
                       RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
-        std::vector<int> redo;  // fp32 bottom blocks above the trace bound (slot bit 1)
-        for (int b = 0; b < count; ++b)
-            if (st_h[b] == 0 && (wide_h[b] & 2)) redo.push_back(b);
-        if (!redo.empty() && est == APM_EST_IS) {
-            bottom64_rerun(c, count, redo);
+        const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
+        std::vector<int> redo, rewrite;  // fp32 bottom blocks above the trace bound (bit 1);
+        bool attached = false;           // wide slots whose fp64 factor was not written (bit 2)
+        for (int b = 0; b < count; ++b) {
+            if (st_h[b] != 0) continue;
+            const bool rd = (wide_h[b] & 2) && est == APM_EST_IS;
+            if (rd) redo.push_back(b);
+            if ((wide_h[b] & 4) && !c->l64_h[hs[b]]) {
+                attach_l64(c, hs[b]);
+                attached = true;
+                if (!rd) rewrite.push_back(b);
+            }
+        }
+        if (attached) upload_l64(c);
+        if (!redo.empty()) bottom64_rerun(c, count, redo);  // (writes the wide ones' fp64 factor)
+        if (!rewrite.empty()) {
+            if (!redo.empty()) sync(c);  // (hmask feeds bottom64_rerun's pending copy)
+            for (int b = 0; b < count; ++b) c->hmask[b] = 0;
+            for (int b : rewrite) c->hmask[b] = 1;
+            HIPC(hipMemcpyAsync(c->active2, c->hmask, sizeof(int) * count, hipMemcpyHostToDevice,
+                                c->stream));
+            launch_slot_write_L64(c->A, c->Sl, c->d_slots, est == APM_EST_PRIORMC ? 1 : 2, c->np,
+                                  Live{c->active2, c->status}, count, c->stream);
+            check_launch();
+        }
+        if (!redo.empty() || !rewrite.empty()) {
             u_eval_device(c, count, true);
             read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
                           RB{c->status, (int)sizeof(int) * count, st_h.data()},
                           RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
         }
-        const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
-        for (int b = 0; b < count; ++b)
-            if (st_h[b] == 0) c->slot_wide[hs[b]] = wide_h[b] & 1;
+        bool detached = false;
+        for (int b = 0; b < count; ++b) {
+            if (st_h[b] != 0) continue;
+            c->slot_wide[hs[b]] = wide_h[b] & 1;
+            if (!(wide_h[b] & 1) && c->l64_h[hs[b]]) {
+                detach_l64(c, hs[b]);
+                detached = true;
+            }
+        }
+        if (detached) upload_l64(c);
     }
     for (int b = 0; b < count; ++b) {
         status[b] = st_h[b];
@@ -1034,6 +1086,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     // development knobs, read here once per context; defaults are the measured best
     if (const char* e = getenv("APM_OUTER")) c->outer = std::max(1, atoi(e));
     HIPC(hipSetDevice(device));
+    trsv32_mw_init();
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
     if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
@@ -1130,9 +1183,12 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->Sl = SlotSet{dalloc<float>(c, n_slots * Lsz), dalloc<double>(c, n_slots * np),
                     dalloc<double>(c, n_slots * np), dalloc<double>(c, n_slots * np),
                     dalloc<double>(c, n_slots), Lsz, np,
-                    dalloc<double>(c, n_slots * np * np), dalloc<double>(c, n_slots * np),
-                    dalloc<int>(c, n_slots), dalloc<int>(c, B), np * np, APM_WIDE_Q,
-                    APM_POST32_Q};
+                    nullptr, dalloc<double>(c, n_slots * np), dalloc<int>(c, n_slots),
+                    dalloc<int>(c, B), APM_WIDE_Q, APM_POST32_Q};
+    c->l64_d = dalloc<double*>(c, n_slots);
+    c->Sl.L64 = c->l64_d;
+    c->l64_h.assign((size_t)n_slots, nullptr);
+    HIPC(hipMemset(c->l64_d, 0, sizeof(double*) * n_slots));
     if (const char* e = getenv("APM_WIDE_Q")) c->Sl.wide_q = atof(e);  // development knob
     if (const char* e = getenv("APM_POST32_Q")) c->Sl.post_q = atof(e);
     c->Sl.post_q = std::min(c->Sl.post_q, c->Sl.wide_q);  // (a wide slot needs the fp64 factor)

@@ -1414,19 +1414,20 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
 
 bool trsv32_mw_ok(int np) { return np <= TRF_MAXNP; }
 
+// dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP); apm_create calls it with the
+// context's device current
+void trsv32_mw_init() {
+    const int mx = (int)(sizeof(double) * (TRF_MAXNP + 4 * 64 + 64));
+    (void)hipFuncSetAttribute((const void*)k_trsv32_mw<true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    (void)hipFuncSetAttribute((const void*)k_trsv32_mw<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+}
+
 void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
                       int fail_code, hipStream_t s) {
     const size_t lds = sizeof(double) * (nb * 64 + 4 * 64 + 64);
-    static bool attr = false;
-    if (!attr) {  // dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP)
-        const int mx = (int)(sizeof(double) * (TRF_MAXNP + 4 * 64 + 64));
-        (void)hipFuncSetAttribute((const void*)k_trsv32_mw<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        (void)hipFuncSetAttribute((const void*)k_trsv32_mw<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        attr = true;
-    }
     const int np = nb * 64;
     const int G = TRM_G;
     hipLaunchKernelGGL(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,

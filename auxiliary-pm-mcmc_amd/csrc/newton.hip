@@ -319,10 +319,12 @@ __global__ __launch_bounds__(256) void k_slot_write_L64(MatB A, SlotSet S,
                                                         int mode, int np, Live live) {
     const int b = blockIdx.y;
     if (live.status[b] != 0 || live.active[b] == 0 || !S.wide[slots[b]] || mode == 3) return;
+    double* const L0 = S.L64[slots[b]];
+    if (!L0) return;  // no buffer yet: the host attaches one and writes the slot again
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = blockIdx.x * 4 + w;  // 0 .. np-1
     const double* Ab = A.base + b * A.cstride;
-    double* L = S.L64 + slots[b] * S.l64stride + (int64_t)r * np;
+    double* L = L0 + (int64_t)r * np;
     const int cend = (r / 64 + 1) * 64;  // as k_slot_write_L: k_ugemm64 reads no further
     if (mode == 2) {
         const double* src = Ab + ((int64_t)np + r) * A.ld;
@@ -364,9 +366,11 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
     tq = block_sum_d(tq, red);
     if (threadIdx.x == 0) {
         // (an fp32 bottom block above post_q is recomputed in fp64 and rewritten in mode 2)
+        // bit 0: wide now; bit 1: fp32 bottom to recompute; bit 2: wide once it is (the host
+        // attaches an fp64 buffer to the slot of every chain with bit 2)
         const int wd = tq > S.wide_q && mode != 3 ? 1 : 0;
         S.wide[slots[b]] = wd;
-        S.chain_wide[b] = wd | (mode == 3 && tq > S.post_q ? 2 : 0);
+        S.chain_wide[b] = wd | (mode == 3 && tq > S.post_q ? 2 : 0) | (tq > S.wide_q ? 4 : 0);
         double c = 0.0;
         if (mode != 1) {
             double ld = 0.0;
@@ -384,6 +388,11 @@ void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride
                        mode, np, v.Kb, v.vstride, live, S32);
     hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
+    launch_slot_write_L64(A, S, slots, mode, np, live, nchains, s);
+}
+
+void launch_slot_write_L64(MatB A, SlotSet S, const int64_t* slots, int mode, int np, Live live,
+                           int nchains, hipStream_t s) {
     hipLaunchKernelGGL(k_slot_write_L64, dim3(np / 4, nchains), dim3(256), 0, s, A, S, slots, mode,
                        np, live);
 }

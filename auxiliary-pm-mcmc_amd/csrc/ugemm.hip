@@ -288,7 +288,8 @@ __global__ __launch_bounds__(256) void k_ugemm64(SlotSet S, const int64_t* __res
     __shared__ double La[64][17];
     __shared__ double Ub[16][65];
     __shared__ double csum[2][64];
-    const double* L = S.L64 + slot * S.l64stride;
+    const double* L = S.L64[slot];
+    if (!L) return;  // wide by this call, buffer not attached yet: recomputed after it is
     const double* U = P.base + ubufs[b] * P.stride;
     const int sp = P.sp;
     d4_t acc[2][2];

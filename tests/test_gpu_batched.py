@@ -170,3 +170,57 @@ def test_batched_pmmh_laplace_phase_matches_api_sampler(gpu_available):
     th1, nrej1 = one.get_samples(6, th0[1:2])
     np.testing.assert_array_equal(th1[0], th2[1])
     assert nrej1[0] == nrej2[1]
+
+
+def test_batched_mi_rdss_consistent_batch_invariant_and_async(gpu_available, tmp_path):
+    """APMMetIndPlusRandDirSliceSampler (samplers.py:926-1004) batched: consistent current state
+    against the oracle, async == lockstep bit for bit, each chain's trajectory independent of
+    its batch (first_chain), and checkpoint / restore replaying the accepted MI draws."""
+    from auxpm.batched import BatchedAPMMetIndPlusRandDirSliceSampler as S
+    X, y, prior = _data()
+    a = S(X, y, 4, 16, prior, seed=51)
+    b = S(X, y, 4, 16, prior, seed=51)
+    a.initialise()
+    lock = np.stack([a.step() for _ in range(4)], 1)
+    assert not a.failed.any()
+    assert (a.n_reject_u < 4).any() and (a.n_reject_u > 0).any()  # MI moves accepted / rejected
+    _current_state_consistent(a, X, y, prior)
+    b.initialise()
+    traces, done = b.run_async(4)
+    np.testing.assert_array_equal(np.array(traces), lock)
+    np.testing.assert_array_equal(a.log_f, b.log_f)
+    np.testing.assert_array_equal(a.n_reject_u, b.n_reject_u)
+    one = S(X, y, 1, 16, prior, seed=51, first_chain=3)
+    one.initialise()  # chain 3's own stream: the same prior draw
+    tr1, _ = one.run_async(3)
+    np.testing.assert_array_equal(np.array(tr1[0]), lock[3, 0:3])
+    np.savez(tmp_path / 'ck.npz', **a.checkpoint())
+    ta, _ = a.run_async(2)
+    c = S(X, y, 4, 16, prior, seed=51)
+    with np.load(tmp_path / 'ck.npz') as z:
+        assert c.restore({k: z[k] for k in z.files}) == 0.
+    tc, _ = c.run_async(2)
+    np.testing.assert_array_equal(np.array(ta), np.array(tc))
+
+
+def test_batched_mi_mh_consistent_and_batch_invariant(gpu_available):
+    """APMMetIndPlusMHSampler (samplers.py:265-418) batched: (n_reject_u, n_reject_theta) per
+    chain like the reference's tuple, consistent state, batch invariance, and the adaptive run
+    driven by the theta rejections (reject_count_index=1)."""
+    from auxpm.batched import BatchedAPMMetIndPlusMHSampler as S
+    X, y, prior = _data()
+    th0 = np.tile(np.r_[0.0, np.full(4, np.log(2.))], (4, 1))
+    smp = S(X, y, 4, 16, prior, prop_scales=0.1, seed=61)
+    th, (nru, nrt) = smp.get_samples(6, th0)
+    assert np.isfinite(th).all() and not smp.failed.any()
+    assert (nru < 5).any() and (nrt < 5).any()
+    _current_state_consistent(smp, X, y, prior)
+    one = S(X, y, 1, 16, prior, prop_scales=0.1, seed=61, first_chain=1)
+    th1, (nru1, nrt1) = one.get_samples(6, th0[1:2])
+    np.testing.assert_array_equal(th1[0], th[1])
+    assert nru1[0] == nru[1] and nrt1[0] == nrt[1]
+    with pytest.raises(ValueError):
+        smp.adaptive_run(th[:, -1], 3, 1, 0.15, 0.30, lambda b, n: 1.5)
+    ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5,
+                                      reject_count_index=1)
+    assert ath.shape == (4, 8, smp.P) and sc.shape == (4, 2, smp.P)

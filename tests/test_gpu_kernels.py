@@ -155,6 +155,46 @@ def test_wide_slot_fp64_path_vs_golden(nat, monkeypatch):
             assert abs(w - f) <= 1e-4, (ci, w, f)
 
 
+def test_wide_buffers_follow_slots(nat, monkeypatch):
+    """fp64 factors are attached to slots only while they are wide (capi.cpp attach_l64 /
+    detach_l64): a slot that turns narrow gives its buffer back, the next wide slot takes it, and
+    every cached u-call afterwards equals a fresh context's - in a batch of wide and narrow
+    chains, across the IS (fp32 bottom + fp64 rerun) and PriorMC writers."""
+    c = _cases()[0]
+    th_n = c['theta'].copy()
+    th_w = c['theta'].copy()
+    th_w[0] = th_n[0] + 4.0  # trace(C) 23 -> 724, trace(K) 81 -> 4422 (oracle): bound 300
+    monkeypatch.setenv('APM_WIDE_Q', '300')
+    ctx = _ctx(nat, c, max_batch=2, n_slots=3, n_ubufs=2)
+    fresh = _ctx(nat, c, max_batch=1, n_slots=1, n_ubufs=2)
+    monkeypatch.delenv('APM_WIDE_Q')
+    for x in (ctx, fresh):
+        x.u_upload(0, c['ns1'])
+        x.u_upload(1, c['ns2'])
+
+    def one(est, th):
+        o, st, _ = fresh.theta_eval(est, th[None], [0], [0])
+        u, _ = fresh.u_eval([0], [1])
+        assert st[0] == 0
+        return o[0], u[0]
+    seq = [((nat.EST_IS, nat.EST_IS), (th_w, th_n), (0, 1)),
+           ((nat.EST_IS, nat.EST_IS), (th_n, th_w), (0, 2)),
+           ((nat.EST_PRIORMC, nat.EST_IS), (th_w, th_w), (1, 0)),
+           ((nat.EST_IS, nat.EST_PRIORMC), (th_n, th_n), (1, 2))]
+    for ests, ths, slots in seq:
+        for e, th, sl in zip(ests, ths, slots):
+            o, st, _ = ctx.theta_eval(e, th[None], [0], [sl])
+            assert st[0] == 0
+            u, _ = ctx.u_eval([sl], [1])
+            fo, fu = one(e, th)
+            assert o[0] == fo and u[0] == fu, (e, sl, o[0], fo, u[0], fu)
+        u2, _ = ctx.u_eval(list(slots), [1, 1])  # both slots in one cached call
+        for q, (e, th) in enumerate(zip(ests, ths)):
+            assert u2[q] == one(e, th)[1]
+    ctx.close()
+    fresh.close()
+
+
 def test_cache_tuple_vs_golden(nat):
     """Iterating the API's IS cache yields the reference's (K_chol, C_chol, f_post) tuple
     (estimators.py:166-176); a PriorMC cache converts to the reference's K_chol array
