@@ -8,7 +8,8 @@ estimators (gpdemo.estimators -> libapm.so) reproduce chains of the reference.
   threshold: the traces must agree to 1e-6 and n_cubic_ops exactly.
 * test_config1_ess_mh_chain_matches_oracle: BASELINE.json configs[1] shape (Pima-sized N=768,
   D=8, ARD-SE, APM with E-SS on u + MH on theta, N_imp=64): GPU estimator vs the oracle's CPU
-  restatement of the reference estimator, driven by the same sampler and seed.
+  restatement of the reference estimator, driven by the same sampler and seed, and vs the
+  reference's own chain (tests/golden/config1_ref.npz).
 """
 import numpy as np
 import pytest
@@ -29,6 +30,11 @@ def nat(gpu_available):
     from gpdemo import _native
     _native.load_library()
     return _native
+
+
+def _x_sha256(X):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(X, dtype=np.float64).tobytes()).hexdigest()
 
 
 def _closure(e, P, prior):
@@ -93,3 +99,11 @@ def test_config1_ess_mh_chain_matches_oracle(nat):
     assert nrej_g == nrej_c
     assert nrej_g < n_sample - 1  # the chain moved: the comparison covers accepted proposals
     np.testing.assert_allclose(th_g, th_c, rtol=1e-10, atol=1e-10)
+    # ... and the REFERENCE's own chain with this wiring (tests/golden/make_golden_config1.py:
+    # reference sampler + reference estimator, same data, seeds and draws)
+    g = golden('config1_ref')
+    assert str(g['x_sha256']) == _x_sha256(X)
+    np.testing.assert_array_equal(y, g['y'])
+    assert nrej_g == int(g['n_reject'])
+    np.testing.assert_allclose(th_g, g['thetas'], rtol=1e-9, atol=1e-9)
+    assert e_gpu.n_cubic_ops == int(g['n_cubic_ops'])

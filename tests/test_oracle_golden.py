@@ -179,3 +179,37 @@ def test_philox_known_answers():
     for inp, out in orc.PHILOX_KAT:
         np.testing.assert_array_equal(orc.philox4x32_10(inp[:4], inp[4:])[0],
                                       np.array(out, dtype=np.uint32))
+
+
+def test_config1_chain_oracle_equals_reference():
+    """BASELINE configs[1] (E-SS + MH, ARD-SE, N=768 D=8, N_imp=64): the API sampler over the
+    oracle's CPU estimator reproduces the reference's own chain (tests/golden/config1_ref.npz,
+    make_golden_config1.py: reference sampler + reference estimator, same data, seeds, draws)."""
+    import hashlib
+    import auxpm.samplers as smp
+    import gpdemo.utils as utils
+    g = golden('config1_ref')
+    n, d, s = 768, 8, 64
+    X, y = utils.synthetic_gp_data(n, d, 1)
+    assert hashlib.sha256(np.ascontiguousarray(X, np.float64).tobytes()).hexdigest() == \
+        str(g['x_sha256'])
+    np.testing.assert_array_equal(y, g['y'])
+    P = d + 1
+    prior = dict(a_tau=1., b_tau=1. / d ** 0.5, a_sigma=1.1, b_sigma=0.1)
+    e = orc.ISEstimatorCPU(X, y, orc.make_kernel_func('ard', 1e-8))
+
+    def log_f(u, theta=None, cached_res=None):
+        val, new_cache = e(u, theta, cached_res)
+        lp = utils.log_gamma_log_pdf(theta[0], prior['a_sigma'], prior['b_sigma'])
+        for k in range(1, P):
+            lp += utils.log_gamma_log_pdf(theta[k], prior['a_tau'], prior['b_tau'])
+        return val + lp, new_cache
+    prng = np.random.RandomState(4321)
+    sampler = smp.APMEllSSPlusMHSampler(
+        log_f, lambda xp, xc, sc: -0.5 * np.sum(((xp - xc) / sc) ** 2),
+        lambda x, sc: x + sc * prng.normal(size=x.shape), np.full(P, 0.05),
+        lambda: prng.normal(size=(n, s)), prng)
+    th, nrej = sampler.get_samples(g['theta_init'], g['thetas'].shape[0])
+    assert nrej == int(g['n_reject'])
+    np.testing.assert_allclose(th, g['thetas'], rtol=1e-10, atol=1e-10)
+    assert e.n_cubic_ops == int(g['n_cubic_ops'])
