@@ -26,6 +26,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'auxiliary-pm-mcmc_amd'))
 
 
+def lib_digest(native):
+    """SHA-256 (16 hex) of the libapm.so this segment ran on."""
+    import hashlib
+    path = os.path.abspath(native.LIB_PATH)
+    with open(path, 'rb') as f:
+        return {'path': os.path.relpath(path, REPO), 'sha16': hashlib.sha256(f.read()).hexdigest()[:16]}
+
+
 def load_series(dirs):
     """All segments' draws, in segment order: (C, T, P) float64."""
     files = {}
@@ -98,6 +106,9 @@ def main():
     ap.add_argument('--d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
+    ap.add_argument('--restore-tol', type=float, default=1e-9,
+                    help='largest |d log f| accepted on resume (a different build of libapm.so '
+                         'continues the chains with its own rounding: ~1e-5 nats)')
     a = ap.parse_args()
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
     from gpdemo.utils import synthetic_gp_data
@@ -126,7 +137,7 @@ def main():
         restore_dlogf = smp.restore(ck)
         print('resumed at {0} transitions per chain; max |d log f| on restore {1:.3g} ({2:.0f} s)'
               .format(have, restore_dlogf, time.perf_counter() - t_start), file=sys.stderr, flush=True)
-        if not restore_dlogf <= 1e-9:
+        if not restore_dlogf <= a.restore_tol:
             raise RuntimeError('restored chains differ from the checkpoint: {0}'.format(restore_dlogf))
     else:
         smp.initialise()
@@ -158,6 +169,8 @@ def main():
     meta['seg_walls'].append(wall)
     meta['seg_transitions'].append(int(done_here * len(live)))
     meta.setdefault('restore_dlogf', []).append(restore_dlogf)
+    from gpdemo import _native
+    meta.setdefault('libs', []).append(lib_digest(_native))
     np.save(os.path.join(a.out_dir, 'series_seg{0:02d}.npy'.format(n_seg)),
             np.array(seg, dtype=np.float32))
     ck = smp.checkpoint()
@@ -168,6 +181,7 @@ def main():
     series, _ = load_series(dirs + [a.out_dir])
     out = summarise(series, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
     out['restore_max_abs_dlogf'] = meta['restore_dlogf']
+    out['segment_libs'] = meta.get('libs')
     with open(os.path.join(a.out_dir, 'summary.json'), 'w') as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ('transitions_per_chain', 'rhat_max', 'rhat_median',
