@@ -498,22 +498,29 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
     def run_async(self, n_steps, keep_going=False, on_round=None):
         """Advance every live chain by at least ``n_steps`` transitions (a number, or one per
         chain) with the asynchronous schedule. keep_going=False: a chain stops after n_steps
-        (the call ends with every chain at a transition boundary); True: chains that are ahead keep working until the slowest
-        has n_steps (throughput mode; a final partial transition is discarded).
-        Returns (traces, done): per chain the list of thetas after each completed transition and
-        the number of completed transitions. on_round(done): called after every batched
-        theta-call (progress reporting)."""
+        (the call ends with every chain at a transition boundary); True: chains that are ahead
+        keep working until the slowest has n_steps (throughput mode; a final partial transition
+        is discarded); 'finish': as True, then the transitions in progress are completed, so
+        every chain ends at a transition boundary with >= n_steps transitions (throughput mode
+        for checkpointed runs). Returns (traces, done): per chain the list of thetas after each
+        completed transition and the number of completed transitions. on_round(done): called
+        after every batched theta-call (progress reporting)."""
         C = self.n_chains
         n_steps = np.broadcast_to(np.asarray(n_steps, dtype=np.int64), (C,))  # or per chain
         done = np.zeros(C, dtype=np.int64)
         traces = [[] for _ in range(C)]
         need_u = ~self.failed
         in_rd = np.zeros(C, dtype=bool)
+        finishing = False
         while True:
             unfinished = (~self.failed) & (done < n_steps)
             if not unfinished.any():
-                break
-            go = (~self.failed) & (unfinished if not keep_going else True)
+                if keep_going != 'finish':
+                    break
+                finishing = True  # no new transitions; complete the ones in progress
+                if not (in_rd & ~self.failed).any():
+                    break
+            go = (~self.failed) & (unfinished if not keep_going else True) & (not finishing)
             ess = np.flatnonzero(need_u & go)
             if ess.size:
                 self._u_update(ess)

@@ -224,3 +224,23 @@ def test_batched_mi_mh_consistent_and_batch_invariant(gpu_available):
     ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5,
                                       reject_count_index=1)
     assert ath.shape == (4, 8, smp.P) and sc.shape == (4, 2, smp.P)
+
+
+def test_run_async_finish_mode_ends_on_boundaries(gpu_available, tmp_path):
+    """keep_going='finish' (tools/ess_long.py's throughput mode): chains that are ahead keep
+    working until the slowest has n_steps, then every transition in progress is completed - so
+    each chain ends at a transition boundary (>= n_steps transitions, traces = done) and a
+    checkpoint taken there continues bit for bit."""
+    _, _, _, a = _sampler(seed=71, chains=4)
+    a.initialise()
+    tr, done = a.run_async(3, keep_going='finish')
+    assert (done >= 3).all() and all(len(t) == d for t, d in zip(tr, done))
+    for c in range(4):
+        np.testing.assert_array_equal(tr[c][-1], a.theta[c])
+    np.savez(tmp_path / 'ck.npz', **a.checkpoint())
+    ta, da = a.run_async(2)
+    _, _, _, b = _sampler(seed=71, chains=4)
+    with np.load(tmp_path / 'ck.npz') as z:
+        assert b.restore({k: z[k] for k in z.files}) == 0.
+    tb, db = b.run_async(2)
+    np.testing.assert_array_equal(np.array(ta), np.array(tb))

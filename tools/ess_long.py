@@ -35,19 +35,27 @@ def lib_digest(native):
 
 
 def load_series(dirs):
-    """All segments' draws, in segment order: (C, T, P) float64."""
+    """All segments' draws per chain, in segment order: a list of (T_c, P) float64 arrays
+    (segments run in the 'finish' throughput mode hold ragged rows, padded with NaN)."""
     files = {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, 'series_seg*.npy')):
             files[os.path.basename(f)] = f
     parts = [np.load(files[k]) for k in sorted(files)]
-    return (np.concatenate(parts, axis=1).astype(np.float64) if parts else None), len(parts)
+    if not parts:
+        return None, 0
+    chains = []
+    for c in range(parts[0].shape[0]):
+        rows = [p[c][~np.isnan(p[c]).any(axis=1)] for p in parts]
+        chains.append(np.concatenate(rows, axis=0).astype(np.float64))
+    return chains, len(parts)
 
 
-def summarise(series, live, warmup, seg_walls, seg_transitions, cfg):
+def summarise(chains, live, warmup, seg_walls, seg_transitions, cfg):
     from auxpm.diagnostics import effective_size, gelman_rubin
-    T = series.shape[1]
-    kept = series[live, warmup:T]
+    T = min(chains[c].shape[0] for c in live)  # common length of the live chains
+    series = np.stack([chains[c][:T] for c in range(len(chains)) if c in set(live)])
+    kept = series[:, warmup:T]
     keep = kept.shape[1]
     traj = []
     step = 500
@@ -68,8 +76,9 @@ def summarise(series, live, warmup, seg_walls, seg_transitions, cfg):
                 'checkpointed segments on one MI355X',
         'config': cfg,
         'segments': len(seg_walls),
-        'failed_chains': int(series.shape[0] - len(live)),
+        'failed_chains': int(len(chains) - len(live)),
         'transitions_per_chain': int(T), 'warmup_discarded': int(warmup), 'kept_per_chain': int(keep),
+        'transitions_per_chain_max': int(max(chains[c].shape[0] for c in live)),
         'sampling_wall_s': wall,
         'transitions_per_s_sampling': tps,
         'ess_min_per_chain_mean': float(ess.min(1).mean()),
@@ -123,7 +132,8 @@ def main():
         seed=a.seed + 1)
     dirs = [a.resume_dir] if a.resume_dir else []
     prev, n_seg = load_series(dirs)
-    have = 0 if prev is None else prev.shape[1]
+    have = np.zeros(a.chains, dtype=np.int64) if prev is None else \
+        np.array([x.shape[0] for x in prev], dtype=np.int64)
     meta = {'seg_walls': [], 'seg_transitions': []}
     restore_dlogf = None
     if a.resume_dir:
@@ -131,55 +141,68 @@ def main():
             ck = {k: z[k] for k in z.files}
         with open(os.path.join(a.resume_dir, 'meta.json')) as f:
             meta = json.load(f)
-        if int(ck['transitions_per_chain']) != have:
+        ck_have = np.broadcast_to(np.asarray(ck['transitions_per_chain'], np.int64), have.shape)
+        if not np.array_equal(ck_have, have):
             raise RuntimeError('checkpoint at {0} transitions, series hold {1}'.format(
-                int(ck['transitions_per_chain']), have))
+                ck_have.tolist(), have.tolist()))
         restore_dlogf = smp.restore(ck)
         print('resumed at {0} transitions per chain; max |d log f| on restore {1:.3g} ({2:.0f} s)'
-              .format(have, restore_dlogf, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+              .format(int(have.min()), restore_dlogf, time.perf_counter() - t_start),
+              file=sys.stderr, flush=True)
         if not restore_dlogf <= a.restore_tol:
             raise RuntimeError('restored chains differ from the checkpoint: {0}'.format(restore_dlogf))
     else:
         smp.initialise()
     seg = [[] for _ in range(a.chains)]
     t0 = time.perf_counter()
-    done_here = 0
+    done_here = np.zeros(a.chains, dtype=np.int64)
     last = 0.0  # duration of the previous chunk: no chunk is started that would overrun
-    while have + done_here < a.target and time.perf_counter() - t0 + last < a.max_seconds:
+    cur = have.copy()
+
+    def slowest():  # the live chains' smallest count (failed chains stop where they failed)
+        live = ~smp.failed
+        return int(cur[live].min()) if live.any() else a.target
+    while slowest() < a.target and time.perf_counter() - t0 + last < a.max_seconds:
         tc = time.perf_counter()
-        step = min(a.chunk, a.target - have - done_here)
+        # every chain to (at least) the slowest one's count + chunk: chains that are ahead keep
+        # working while the batch waits for the slowest ('finish' throughput mode)
+        step = np.maximum(min(slowest() + a.chunk, a.target) - cur, 0)
         beat = [time.perf_counter()]
 
         def heartbeat(done):  # a line a minute inside long chunks (gpurun's hang detection)
             if time.perf_counter() - beat[0] > 60:
                 beat[0] = time.perf_counter()
-                print('  ... chunk: slowest chain {0} / {1}'.format(int(done.min()), step),
+                print('  ... chunk: {0} of {1} chains at their target'.format(
+                    int((done >= step).sum()), len(done)),
                       file=sys.stderr, flush=True)
-        tr, done = smp.run_async(step, on_round=heartbeat)
+        tr, done = smp.run_async(step, keep_going='finish', on_round=heartbeat)
         for c in range(a.chains):
-            if smp.failed[c]:
-                tr[c] = tr[c] + [smp.theta[c].copy()] * (step - len(tr[c]))
             seg[c].extend(tr[c])
-        done_here += step
+        done_here += done
+        cur = have + done_here
         last = time.perf_counter() - tc
-        print('{0} / {1} transitions per chain, segment {2:.0f} s'.format(
-            have + done_here, a.target, time.perf_counter() - t0), file=sys.stderr, flush=True)
+        print('{0} .. {1} / {2} transitions per chain, segment {3:.0f} s'.format(
+            int(cur.min()), int(cur.max()), a.target, time.perf_counter() - t0),
+            file=sys.stderr, flush=True)
     wall = time.perf_counter() - t0
     live = [c for c in range(a.chains) if not smp.failed[c]]
     meta['seg_walls'].append(wall)
-    meta['seg_transitions'].append(int(done_here * len(live)))
+    meta['seg_transitions'].append(int(done_here[live].sum()))
     meta.setdefault('restore_dlogf', []).append(restore_dlogf)
     from gpdemo import _native
     meta.setdefault('libs', []).append(lib_digest(_native))
-    np.save(os.path.join(a.out_dir, 'series_seg{0:02d}.npy'.format(n_seg)),
-            np.array(seg, dtype=np.float32))
+    arr = np.full((a.chains, max(1, max(len(x) for x in seg)), smp.P), np.nan, dtype=np.float32)
+    for c in range(a.chains):
+        if seg[c]:
+            arr[c, :len(seg[c])] = np.array(seg[c], dtype=np.float32)
+    np.save(os.path.join(a.out_dir, 'series_seg{0:02d}.npy'.format(n_seg)), arr)
     ck = smp.checkpoint()
-    ck['transitions_per_chain'] = np.int64(have + done_here)
+    ck['transitions_per_chain'] = (have + done_here).astype(np.int64)
     np.savez(os.path.join(a.out_dir, 'state.npz'), **ck)
     with open(os.path.join(a.out_dir, 'meta.json'), 'w') as f:
         json.dump(meta, f)
-    series, _ = load_series(dirs + [a.out_dir])
-    out = summarise(series, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
+    chains, _ = load_series(dirs + [a.out_dir])
+    out = summarise(chains, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
     out['restore_max_abs_dlogf'] = meta['restore_dlogf']
     out['segment_libs'] = meta.get('libs')
     with open(os.path.join(a.out_dir, 'summary.json'), 'w') as f:
