@@ -110,7 +110,11 @@ def main():
     ap.add_argument('--chunk', type=int, default=100)
     ap.add_argument('--max-seconds', type=float, default=1000.)
     ap.add_argument('--resume-dir', default=None)
-    ap.add_argument('--out-dir', required=True)
+    ap.add_argument('--out-dir', default=None)
+    ap.add_argument('--summarise', default=None, metavar='DIR',
+                    help='no sampling: rewrite DIR/summary.json from every series_seg*.npy, '
+                         'meta.json and state.npz in DIR (CPU only; a resume directory may hold '
+                         'the state alone, so that only it travels to the GPU box)')
     ap.add_argument('--n', type=int, default=4096)
     ap.add_argument('--d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
@@ -119,14 +123,29 @@ def main():
                     help='largest |d log f| accepted on resume (a different build of libapm.so '
                          'continues the chains with its own rounding: ~1e-5 nats)')
     a = ap.parse_args()
+    cfg = {'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'chains': a.chains,
+           'seed': a.seed, 'kernel': 'ard', 'epsilon': 1e-8, 'w': 1., 'max_steps_out': 0}
+    if a.summarise:
+        with open(os.path.join(a.summarise, 'meta.json')) as f:
+            meta = json.load(f)
+        chains, _ = load_series([a.summarise])
+        with np.load(os.path.join(a.summarise, 'state.npz')) as z:
+            failed = z['failed'] if 'failed' in z.files else np.zeros(len(chains), bool)
+        live = [c for c in range(len(chains)) if not failed[c]]
+        out = summarise(chains, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
+        out['restore_max_abs_dlogf'] = meta['restore_dlogf']
+        out['segment_libs'] = meta.get('libs')
+        with open(os.path.join(a.summarise, 'summary.json'), 'w') as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps({k: out[k] for k in ('transitions_per_chain', 'rhat_max', 'rhat_median',
+                                              'ess_per_transition_min_component')}))
+        return
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
     from gpdemo.utils import synthetic_gp_data
     os.makedirs(a.out_dir, exist_ok=True)
     t_start = time.perf_counter()
     X, y = synthetic_gp_data(a.n, a.d, a.seed)
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
-    cfg = {'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'chains': a.chains,
-           'seed': a.seed, 'kernel': 'ard', 'epsilon': 1e-8, 'w': 1., 'max_steps_out': 0}
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
         seed=a.seed + 1)
@@ -141,7 +160,10 @@ def main():
             ck = {k: z[k] for k in z.files}
         with open(os.path.join(a.resume_dir, 'meta.json')) as f:
             meta = json.load(f)
+        n_seg = len(meta['seg_walls'])  # (a state-only directory holds no series files)
         ck_have = np.broadcast_to(np.asarray(ck['transitions_per_chain'], np.int64), have.shape)
+        if prev is None:  # a state-only resume directory
+            have = ck_have.copy()
         if not np.array_equal(ck_have, have):
             raise RuntimeError('checkpoint at {0} transitions, series hold {1}'.format(
                 ck_have.tolist(), have.tolist()))
@@ -201,6 +223,10 @@ def main():
     np.savez(os.path.join(a.out_dir, 'state.npz'), **ck)
     with open(os.path.join(a.out_dir, 'meta.json'), 'w') as f:
         json.dump(meta, f)
+    if a.resume_dir and prev is None:  # state-only resume: the summary needs every segment
+        print('segment {0} written; merge it into the full directory and run --summarise'.format(
+            n_seg), file=sys.stderr, flush=True)
+        return
     chains, _ = load_series(dirs + [a.out_dir])
     out = summarise(chains, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
     out['restore_max_abs_dlogf'] = meta['restore_dlogf']
