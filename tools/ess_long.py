@@ -30,6 +30,8 @@ def lib_digest(native):
     """SHA-256 (16 hex) of the libapm.so this segment ran on."""
     import hashlib
     path = os.path.abspath(native.LIB_PATH)
+    if not os.path.exists(path):
+        return {'path': os.path.relpath(path, REPO), 'sha16': None}
     with open(path, 'rb') as f:
         return {'path': os.path.relpath(path, REPO), 'sha16': hashlib.sha256(f.read()).hexdigest()[:16]}
 

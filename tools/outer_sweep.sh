@@ -1,5 +1,5 @@
 # time_theta (64 chains) under several values of blocking / launch-shape knobs (development tool):
-#   bash tools/outer_sweep.sh VAR v1 v2 ...   (VAR: APM_OUTER, APM_OUTER32, APM_TRSV_G, ...)
+#   bash tools/outer_sweep.sh VAR v1 v2 ...   (VAR: APM_OUTER, APM_OVERLAP_K, ... - DESIGN.md §7)
 set -e
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 VAR=$1; shift
