@@ -24,6 +24,11 @@ streams and the masked-failure bookkeeping (``_BatchedChains``):
   :588-710) and ``APMMetIndPlusMHSampler`` (:265-418): the same theta updates, with u updated
   by a Metropolis independence step (mcmc_updates.py:159-303: a fresh u from the device, one
   batched u-call against the current cache, accept iff U < exp(log f' - log f)).
+* ``BatchedAPMMetIndPlusSeqSliceSampler`` — ``APMMetIndPlusSeqSliceSampler`` (:844-923): MI on
+  u, then a linear slice step along each theta axis in turn (widths ``ws``).
+* ``BatchedAPMEllSSPlusEllSSSampler`` — ``APMEllSSPlusEllSSSampler`` (:1092-1165): E-SS on u and
+  E-SS on theta under a zero-mean Gaussian prior (``theta_prior_std``; the log target is the
+  estimate alone, as the reference's estimator there excludes that prior).
 
 Per chain the control flow, the cache protocol and the host-RNG draw order are those of the
 reference (one ``numpy.random.RandomState`` per chain for slice heights, angles, offsets,
@@ -46,7 +51,8 @@ from gpdemo.utils import log_prior_ard_batch
 
 __all__ = ['BatchedAPMEllSSPlusRandDirSliceSampler', 'BatchedAPMEllSSPlusMHSampler',
            'BatchedPMMHSampler', 'BatchedAPMMetIndPlusRandDirSliceSampler',
-           'BatchedAPMMetIndPlusMHSampler', 'chain_streams']
+           'BatchedAPMMetIndPlusMHSampler', 'BatchedAPMMetIndPlusSeqSliceSampler',
+           'BatchedAPMEllSSPlusEllSSSampler', 'chain_streams']
 
 _EST = {'is': _native.EST_IS, 'priormc': _native.EST_PRIORMC, 'laplace': _native.EST_LAPLACE}
 
@@ -339,6 +345,10 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
         self._rd_up = np.zeros(C)
         self._rd_it = np.zeros(C, dtype=np.int64)
         self._rd_pend = np.zeros((C, self.P))
+        # the line of the slice step: theta + x d (axis -1, x_curr = 0) or, for the sequential
+        # sampler, theta with component `axis` set to x (x_curr = that component)
+        self._rd_axis = np.full(C, -1, dtype=np.int64)
+        self._rd_x0 = np.zeros(C)
 
     def _rdss_theta(self):
         """Random-direction linear slice update of every live chain's theta
@@ -422,15 +432,30 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
         return self.theta.copy()
 
     # ------------------------------------------------------------------ asynchronous schedule
+    def _theta_begin(self, c):
+        """Start the theta half of chain c's transition (the MI / seq / ESS twins override)."""
+        self._rd_begin(c)
+
+    def _theta_result(self, c, lf, lp):
+        return self._rd_result(c, lf, lp)
+
     def _rd_begin(self, c):
         """Start chain c's random-direction slice step: the draws of mcmc_updates.py:480-490 in
         the reference order (direction, slice height, bracket offset, step-out split)."""
         rng = self.prngs[c]
         dd = rng.normal(size=self.P)
         self._rd_d[c] = dd / dd.dot(dd) ** 0.5
+        self._rd_axis[c] = -1
+        self._line_begin(c, 0., self.w)
+
+    def _line_begin(self, c, x0, w):
+        """A linear slice step from x0 with bracket width w (mcmc_updates.py:480-490: slice
+        height, bracket offset, step-out split, in the reference's draw order)."""
+        rng = self.prngs[c]
+        self._rd_x0[c] = x0
         self._rd_logy[c] = np.log(rng.uniform()) + self.log_f[c]
-        self._rd_lo[c] = 0. - self.w * rng.uniform()
-        self._rd_hi[c] = self._rd_lo[c] + self.w
+        self._rd_lo[c] = x0 - w * rng.uniform()
+        self._rd_hi[c] = self._rd_lo[c] + w
         self._rd_s[c] = 0
         self._rd_it[c] = 0
         if self.max_steps_out > 0:
@@ -441,21 +466,28 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
             self._rd_mode[c] = 2
         self._rd_next(c)
 
+    def _line_point(self, c, x):
+        if self._rd_axis[c] < 0:
+            return self.theta[c] + x * self._rd_d[c]
+        p = self.theta[c].copy()
+        p[self._rd_axis[c]] = x
+        return p
+
     def _rd_next(self, c):
         """Set chain c's next theta to evaluate (a step-out probe or a shrink proposal)."""
         if self._rd_mode[c] == 0:
             if self._rd_s[c] < self._rd_down[c]:
-                self._rd_pend[c] = self.theta[c] + self._rd_lo[c] * self._rd_d[c]
+                self._rd_pend[c] = self._line_point(c, self._rd_lo[c])
                 return
             self._rd_mode[c], self._rd_s[c] = 1, 0
         if self._rd_mode[c] == 1:
             if self._rd_s[c] < self._rd_up[c]:
-                self._rd_pend[c] = self.theta[c] + self._rd_hi[c] * self._rd_d[c]
+                self._rd_pend[c] = self._line_point(c, self._rd_hi[c])
                 return
             self._rd_mode[c] = 2
         self._rd_x[c] = self._rd_lo[c] + (self._rd_hi[c] - self._rd_lo[c]) * \
             self.prngs[c].uniform()
-        self._rd_pend[c] = self.theta[c] + self._rd_x[c] * self._rd_d[c]
+        self._rd_pend[c] = self._line_point(c, self._rd_x[c])
 
     def _rd_result(self, c, lf, lp):
         """Consume the estimate lf (log prior lp) at chain c's pending theta; True when the
@@ -463,10 +495,11 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
         mode = self._rd_mode[c]
         if mode < 2:  # step out while the bracket end is inside the slice (mcmc_updates.py:491-498)
             if self._rd_logy[c] < lf:
+                w = self.w if self._rd_axis[c] < 0 else self.ws[self._rd_axis[c]]
                 if mode == 0:
-                    self._rd_lo[c] -= self.w
+                    self._rd_lo[c] -= w
                 else:
-                    self._rd_hi[c] += self.w
+                    self._rd_hi[c] += w
                 self._rd_s[c] += 1
             else:
                 self._rd_mode[c], self._rd_s[c] = mode + 1, 0
@@ -480,10 +513,10 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
             return True
         if self.failed[c]:
             return True
-        x = self._rd_x[c]
-        if x < 0.:
+        x, x0 = self._rd_x[c], self._rd_x0[c]
+        if x < x0:
             self._rd_lo[c] = x
-        elif x > 0.:
+        elif x > x0:
             self._rd_hi[c] = x
         else:
             warnings.warn('Slice collapsed to current value')
@@ -527,14 +560,14 @@ class BatchedAPMEllSSPlusRandDirSliceSampler(_BatchedChains):
                 for c in ess:
                     need_u[c] = False
                     if not self.failed[c]:
-                        self._rd_begin(c)
+                        self._theta_begin(c)
                         in_rd[c] = True
             rd = np.flatnonzero(in_rd & ~self.failed)
             if rd.size == 0:
                 break
             lf, lp = self._theta_eval(rd, self._rd_pend[rd], self.slot_prop[rd])
             for q, c in enumerate(rd):
-                if self._rd_result(c, lf[q], lp[q]):
+                if self._theta_result(c, lf[q], lp[q]):
                     in_rd[c] = False
                     if not self.failed[c]:
                         done[c] += 1
@@ -752,3 +785,111 @@ class BatchedAPMMetIndPlusMHSampler(BatchedAPMEllSSPlusMHSampler):
 
     def _rejections(self):
         return self.n_reject_u.copy(), self.n_reject.copy()
+
+
+class BatchedAPMMetIndPlusSeqSliceSampler(BatchedAPMEllSSPlusRandDirSliceSampler):
+    """Batch of APM MI(u) + sequential-axis SS(theta) chains (reference
+    APMMetIndPlusSeqSliceSampler, samplers.py:844-923): after the Metropolis independence
+    u-update, one linear slice step (mcmc_updates.py:403-519) along theta axis j = 0 .. P-1 in
+    turn, from x_curr = theta_j with bracket width ws[j], each axis starting from the previous
+    axis's state and estimate. Same asynchronous schedule (one batched theta-call per round for
+    every chain whose axis step needs an evaluation); ``step()`` is one such transition."""
+
+    def __init__(self, X, y, n_chains, n_imp, prior, ws, kernel='ard', epsilon=1e-8,
+                 max_steps_out=0, max_slice_iters=1000, seed=0, estimator='is', device=None,
+                 first_chain=0):
+        super(BatchedAPMMetIndPlusSeqSliceSampler, self).__init__(
+            X, y, n_chains, n_imp, prior, kernel, epsilon, 1., max_steps_out, max_slice_iters,
+            seed, estimator, device, first_chain)
+        self.ws = np.array(np.broadcast_to(np.asarray(ws, dtype=np.float64), (self.P,)))
+
+    def _u_update(self, chains=None):
+        self._mi_u(chains)
+
+    def _theta_begin(self, c):
+        self._axis_begin(c, 0)
+
+    def _axis_begin(self, c, j):
+        self._rd_axis[c] = j
+        self._line_begin(c, self.theta[c, j], self.ws[j])
+
+    def _theta_result(self, c, lf, lp):
+        if not self._rd_result(c, lf, lp):
+            return False
+        j = self._rd_axis[c]
+        if self.failed[c] or j + 1 >= self.P:
+            return True
+        self._axis_begin(c, j + 1)  # the next axis from the state this one left
+        return False
+
+    def step(self):
+        self.run_async(1)
+        return self.theta.copy()
+
+
+class BatchedAPMEllSSPlusEllSSSampler(BatchedAPMEllSSPlusRandDirSliceSampler):
+    """Batch of APM E-SS(u) + E-SS(theta) chains (reference APMEllSSPlusEllSSSampler,
+    samplers.py:1092-1165): theta has a zero-mean Gaussian prior with per-component standard
+    deviations ``theta_prior_std`` (the reference's theta_sampler draws from it) and the log
+    target the estimator sees excludes it (log prior 0 here). The theta update is the elliptical
+    slice step of mcmc_updates.py:311-400 with nu = theta_prior_std * N(0, I) from the chain's
+    RandomState (drawn first, as samplers.py:1163), on the asynchronous schedule."""
+
+    def __init__(self, X, y, n_chains, n_imp, theta_prior_std, kernel='ard', epsilon=1e-8,
+                 max_slice_iters=1000, seed=0, estimator='is', device=None, first_chain=0):
+        super(BatchedAPMEllSSPlusEllSSSampler, self).__init__(
+            X, y, n_chains, n_imp, {}, kernel, epsilon, 1., 0, max_slice_iters, seed, estimator,
+            device, first_chain)
+        self.theta_prior_std = np.array(np.broadcast_to(
+            np.asarray(theta_prior_std, dtype=np.float64), (self.P,)))
+        C = self.n_chains
+        self._el_v = np.zeros((C, self.P))
+        self._el_phi = np.zeros(C)
+
+    def log_prior(self, thetas):
+        return np.zeros(len(thetas))
+
+    def prior_draw(self):
+        return np.stack([self.theta_prior_std * rng.normal(size=self.P) for rng in self.prngs])
+
+    def _el_point(self, c):
+        phi = self._el_phi[c]
+        return self.theta[c] * np.cos(phi) + self._el_v[c] * np.sin(phi)
+
+    def _theta_begin(self, c):
+        rng = self.prngs[c]
+        self._el_v[c] = self.theta_prior_std * rng.normal(size=self.P)
+        self._rd_logy[c] = self.log_f[c] + np.log(rng.uniform())
+        self._el_phi[c] = rng.uniform() * 2. * np.pi
+        self._rd_lo[c], self._rd_hi[c] = self._el_phi[c] - 2. * np.pi, self._el_phi[c]
+        self._rd_it[c] = 0
+        self._rd_pend[c] = self._el_point(c)
+
+    def _theta_result(self, c, lf, lp):
+        if lf > self._rd_logy[c]:  # accept: the proposal's cache becomes current
+            self.slot_cur[c], self.slot_prop[c] = self.slot_prop[c], self.slot_cur[c]
+            self.theta[c] = self._rd_pend[c]
+            self.log_f[c] = lf
+            self.lp_cur[c] = lp
+            return True
+        if self.failed[c]:
+            return True
+        phi = self._el_phi[c]
+        if phi < 0:
+            self._rd_lo[c] = phi
+        elif phi > 0:
+            self._rd_hi[c] = phi
+        else:
+            warnings.warn('Slice collapsed to current value')
+            return True
+        self._rd_it[c] += 1
+        if self._rd_it[c] >= self.max_slice_iters:
+            self.failed[c] = True
+            return True
+        self._el_phi[c] = self._rd_lo[c] + self.prngs[c].uniform() * (self._rd_hi[c] - self._rd_lo[c])
+        self._rd_pend[c] = self._el_point(c)
+        return False
+
+    def step(self):
+        self.run_async(1)
+        return self.theta.copy()
