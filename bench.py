@@ -550,9 +550,19 @@ def ess_long_record(value, a):
         return None
     ept = r['ess_per_transition_min_component']
     eptm = r.get('ess_per_transition_mean_component')
+    # the record's own sampling rate at stationarity (its chains sit where the posterior puts
+    # them, log sigma ~3.5 here: ~9 Newton iterations per theta-call against ~4 for this run's
+    # prior-initialised chains), on the newest library it ran on
+    lib = r.get('latest_library') or {}
+    tps_st = lib.get('transitions_per_s') or r.get('transitions_per_s_sampling')
     return {'source': os.path.relpath(files[-1], REPO),
             'ess_per_transition_min_component': ept,
             'ess_per_transition_mean_component': eptm,
+            'stationary_transitions_per_s': tps_st,
+            'stationary_library_sha16': lib.get('sha16'),
+            'stationary_posterior_mean_log_sigma': r.get('posterior_mean_log_sigma'),
+            'ess_per_sec_stationary': ept * tps_st if tps_st else None,
+            'ess_mean_per_sec_stationary': eptm * tps_st if tps_st and eptm is not None else None,
             'ess_per_sec_estimate': ept * value,
             'ess_mean_per_sec_estimate': eptm * value if eptm is not None else None,
             'rhat_max': r['rhat_max'], 'rhat_median': r.get('rhat_median'),
@@ -562,7 +572,10 @@ def ess_long_record(value, a):
             'chains': cfg.get('chains'),
             'warmup_discarded': r.get('warmup_discarded', cfg.get('warmup_discarded')),
             'kept_per_chain': r.get('kept_per_chain', cfg.get('kept_per_chain')),
-            'note': 'ESS per transition from the long-chain record x this run\'s transitions/s'}
+            'note': 'ESS per transition from the long-chain record x the record\'s own '
+                    'stationary transitions/s (the headline ess_per_sec) or x this run\'s '
+                    'transitions/s (ess_per_sec_estimate: prior-initialised chains, fewer Newton '
+                    'iterations per theta-call than at stationarity)'}
 
 
 def main():
@@ -833,12 +846,16 @@ def main():
     if lr is not None:  # the headline ESS/s from mixed (or, if not yet, the longest) chains
         line['ess_sample']['ess_per_sec_in_run'] = line['ess_per_sec']
         line['ess_sample']['ess_mean_per_sec_in_run'] = line['ess_mean_per_sec']
-        line['ess_per_sec'] = lr['ess_per_sec_estimate']
-        line['ess_mean_per_sec'] = lr['ess_mean_per_sec_estimate']
+        st = lr['ess_per_sec_stationary'] is not None
+        line['ess_per_sec'] = lr['ess_per_sec_stationary'] if st else lr['ess_per_sec_estimate']
+        line['ess_mean_per_sec'] = (lr['ess_mean_per_sec_stationary'] if st
+                                    else lr['ess_mean_per_sec_estimate'])
         line['ess_per_sec_source'] = (
-            'long-chain record {0}: ESS per transition (min over theta components) x this run\'s '
-            'transitions/s; R-hat max {1:.3f} ({2})'.format(
-                lr['source'], lr['rhat_max'],
+            'long-chain record {0}: ESS per transition (min over theta components) x {1}; R-hat '
+            'max {2:.3f} ({3})'.format(
+                lr['source'], 'the record\'s stationary transitions/s ({0:.1f})'.format(
+                    lr['stationary_transitions_per_s']) if st else 'this run\'s transitions/s',
+                lr['rhat_max'],
                 'converged' if lr['converged_rhat_below_1p1'] else 'NOT converged: R-hat > 1.1'))
     if dist.rank == 0:
         print(json.dumps(line), flush=True)

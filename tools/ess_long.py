@@ -36,6 +36,21 @@ def lib_digest(native):
         return {'path': os.path.relpath(path, REPO), 'sha16': hashlib.sha256(f.read()).hexdigest()[:16]}
 
 
+def library_rate(meta):
+    """Sampling throughput of the segments run on the newest library (meta 'libs' lists the
+    last segments' libraries): the stationary transitions/s of that build."""
+    libs = meta.get('libs') or []
+    if not libs or libs[-1].get('sha16') is None:
+        return {}
+    sha = libs[-1]['sha16']
+    k0 = len(meta['seg_walls']) - len(libs)
+    idx = [k0 + i for i, l in enumerate(libs) if l.get('sha16') == sha]
+    t = sum(meta['seg_transitions'][i] for i in idx)
+    w = sum(meta['seg_walls'][i] for i in idx)
+    return {'latest_library': {'sha16': sha, 'segments': idx, 'transitions': int(t),
+                               'wall_s': w, 'transitions_per_s': t / w if w > 0 else None}}
+
+
 def load_series(dirs):
     """All segments' draws per chain, in segment order: a list of (T_c, P) float64 arrays
     (segments run in the 'finish' throughput mode hold ragged rows, padded with NaN)."""
@@ -73,9 +88,11 @@ def summarise(chains, live, warmup, seg_walls, seg_transitions, cfg):
     tps = ntr / wall if wall > 0 else None
     ept_min = float(ess.min(1).mean() / keep)
     ept_mean = float(ess.mean(1).mean() / keep)
+    seg_tps = [t / w if w > 0 else None for t, w in zip(seg_transitions, seg_walls)]
     return {
         'what': 'long-chain ESS / R-hat at BASELINE configs[2] (SURVEY.md §8d protocol), '
                 'checkpointed segments on one MI355X',
+        'transitions_per_s_by_segment': seg_tps,
         'config': cfg,
         'segments': len(seg_walls),
         'failed_chains': int(len(chains) - len(live)),
@@ -137,6 +154,7 @@ def main():
         out = summarise(chains, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
         out['restore_max_abs_dlogf'] = meta['restore_dlogf']
         out['segment_libs'] = meta.get('libs')
+        out.update(library_rate(meta))
         with open(os.path.join(a.summarise, 'summary.json'), 'w') as f:
             json.dump(out, f, indent=1)
         print(json.dumps({k: out[k] for k in ('transitions_per_chain', 'rhat_max', 'rhat_median',
@@ -233,6 +251,7 @@ def main():
     out = summarise(chains, live, a.warmup, meta['seg_walls'], meta['seg_transitions'], cfg)
     out['restore_max_abs_dlogf'] = meta['restore_dlogf']
     out['segment_libs'] = meta.get('libs')
+    out.update(library_rate(meta))
     with open(os.path.join(a.out_dir, 'summary.json'), 'w') as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ('transitions_per_chain', 'rhat_max', 'rhat_median',
