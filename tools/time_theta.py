@@ -20,6 +20,9 @@ ap.add_argument('--batch', type=int, default=1)
 ap.add_argument('--reps', type=int, default=3)
 ap.add_argument("--no-prof", action="store_true")
 ap.add_argument("--theta0", type=float, default=0.0, help="log signal variance of the thetas")
+ap.add_argument("--theta-file", default=None,
+                help=".npy of (batch, D+1) thetas, e.g. profiles/r04_stationary_thetas.npy (the "
+                     "long-chain record's 64 chains at 9000 transitions: the stationary regime)")
 a = ap.parse_args()
 
 X, y = utils.synthetic_gp_data(a.n, a.d, 20151009)
@@ -28,6 +31,9 @@ ctx = _native.Context(X, y, _native.KERNEL_ARD, 1e-8, a.s, max_batch=a.batch,
 ctx.u_normal(np.arange(a.batch), np.full(a.batch, 7), np.arange(a.batch))
 th = np.tile(np.r_[a.theta0, np.full(a.d, np.log(np.sqrt(a.d)))], (a.batch, 1))
 th += np.random.RandomState(0).normal(scale=0.1, size=th.shape)
+if a.theta_file:
+    th = np.load(a.theta_file)[:a.batch].astype(np.float64)
+    assert th.shape == (a.batch, a.d + 1)
 for r in range(a.reps):
     if r == min(1, a.reps - 1) and not a.no_prof:  # rep 0 is cold (tile lists, first launches): not profiled
         for k in range(_native.PROF_NKINDS):
