@@ -27,7 +27,7 @@ def test_bench_two_ranks_on_one_gpu(gpu_available):
          '--gpus', '2', '--steps', '4', '--warmup', '1', '--chains', '4', '--n-data', '1024',
          '--n-features', '8', '--n-imp', '32', '--cpu-baseline', '0'],
         capture_output=True, text=True, env=env, timeout=500, cwd=REPO)
-    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.returncode == 0, out.stdout[-4000:] + out.stderr[-2000:]
     line = json.loads([l for l in out.stdout.splitlines() if l.startswith('{')][-1])
     assert line['n_gpus'] == 2 and line['config']['global_batch'] == 8
     assert line['failed_chains'] == 0
