@@ -123,10 +123,6 @@ void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double
 // first; fp64 r -> out, r kept); needs np <= 8192 (trsv32_mw_ok), else the per-block steps above
 bool trsv32_mw_ok(int np);
 void trsv32_mw_init();  // per device, once the device is current (apm_create)
-// the same solve by one 1024-thread workgroup per chain (k_trsv32_wg; APM_TRSV_WG)
-void launch_trsv32_wg(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
-                      const double* r, double* out, int64_t vstride, Live live, int nchains,
-                      int fail_code, hipStream_t s);
 void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
                       int fail_code, hipStream_t s);

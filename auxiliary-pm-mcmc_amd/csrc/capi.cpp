@@ -108,9 +108,6 @@ struct apm_ctx {
     // in-panel factorisation of the Newton matrix: one dataflow launch per outer panel
     // (k_chol_panel_df32; APM_DF32=0: the launch sequence it replaces)
     bool df32 = true;
-    // Newton TRSVs by one 1024-thread workgroup per chain (k_trsv32_wg; APM_TRSV_WG=0: the
-    // multi-workgroup k_trsv32_mw)
-    bool trsv_wg = false;
     unsigned long long* dfprog = nullptr;  // per (chain, row tile) progress words
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
@@ -538,8 +535,7 @@ void newton_solve32(apm_ctx* c, int count) {
     const bool mw_trsv = trsv32_mw_ok(np);
     if (mw_trsv) {
         feed_chol_k(c);
-        (c->trsv_wg ? launch_trsv32_wg : launch_trsv32_mw)(false, F, nb, D, ds, r1, c->v.z, vs, lv,
-                                                            count, APM_STATUS_CHOL_B, s);
+        launch_trsv32_mw(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, APM_STATUS_CHOL_B, s);
         check_launch();
     } else {
         for (int J = nb - 1; J >= 0; --J) {
@@ -566,12 +562,10 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         if (mw_trsv) {
             feed_chol_k(c);
-            (c->trsv_wg ? launch_trsv32_wg : launch_trsv32_mw)(true, F, nb, D, ds, r1, r2, vs, lr,
-                                                                count, APM_STATUS_CHOL_B, s);
+            launch_trsv32_mw(true, F, nb, D, ds, r1, r2, vs, lr, count, APM_STATUS_CHOL_B, s);
             check_launch();
             feed_chol_k(c);
-            (c->trsv_wg ? launch_trsv32_wg : launch_trsv32_mw)(false, F, nb, D, ds, r2, r3, vs, lr,
-                                                                count, APM_STATUS_CHOL_B, s);
+            launch_trsv32_mw(false, F, nb, D, ds, r2, r3, vs, lr, count, APM_STATUS_CHOL_B, s);
             check_launch();
         } else {
             for (int J = 0; J < nb; ++J) {
@@ -1098,7 +1092,6 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
-    if (const char* e = getenv("APM_TRSV_WG")) c->trsv_wg = atoi(e) != 0;
     if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;

@@ -1412,157 +1412,11 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
     if (t == 0 && bad) live.status[b] = fail_code;
 }
 
-// ------------------------------------------------------- single-workgroup TRSV (1024 threads/chain)
-// One workgroup of 16 waves per chain keeps the whole solution in LDS: step s (block J = s, or
-// nb-1-s backwards) sums the contributions of the solved blocks - wave w takes the solved blocks
-// idx = w, w+16, ... - into per-wave partials, one wave group forms the step's right-hand side and
-// its product with inv(L_JJ), and two workgroup barriers separate the steps. No inter-workgroup
-// hand-over: the step's critical path is LDS + barriers, and the 16 waves keep many tile loads in
-// flight (the multi-workgroup kernel above hands each step over through global memory).
-// Lane l of a wave covers tile rows 16p + l/4 (p = 0..3) and columns 16(l%4) .. +15: 16-byte
-// loads, 4 lanes per 256-byte row. Fixed summation order per element, so a chain's result does not
-// depend on its batch.
-template <bool FWD>
-__global__ __launch_bounds__(1024) void k_trsv32_wg(MatF A, int nb, const float* Dinv,
-                                                    int64_t dstride, const double* r, double* out,
-                                                    int64_t vstride, Live live, int fail_code) {
-    const int b = blockIdx.x;
-    if (!live32(live, b)) return;
-    extern __shared__ double trw_sm[];
-    double* xs = trw_sm;            // nb*64: the solution
-    double* part = xs + nb * 64;    // 16 waves x 64 partial sums
-    double* rj = part + 16 * 64;    // 64: the step's right-hand side
-    __shared__ int bad;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int sub = lane >> 2, q = lane & 3;
-    if (t == 0) bad = 0;
-    const float* Lb = A.base + b * A.cstride;
-    const float* Db = Dinv + b * dstride;
-    const double* rb = r + b * vstride;
-    double* ob = out + b * vstride;
-    auto blk = [&](int idx) { return FWD ? idx : nb - 1 - idx; };
-    __syncthreads();
-    for (int s = 0; s < nb; ++s) {
-        const int J = blk(s);
-        if (FWD) {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0};
-            for (int idx = w; idx < s; idx += 16) {
-                const int I = blk(idx);
-                const double* x = xs + I * 64 + 16 * q;
-                f4_t v[4][4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        v[p][u] = *reinterpret_cast<const f4_t*>(
-                            Lb + (int64_t)(J * 64 + 16 * p + sub) * A.ld + I * 64 + 16 * q + 4 * u);
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            acc[p] = fma((double)v[p][u][e], x[4 * u + e], acc[p]);
-            }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                acc[p] += __shfl_xor(acc[p], 1, 64);
-                acc[p] += __shfl_xor(acc[p], 2, 64);
-            }
-            if (q == 0) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) part[w * 64 + 16 * p + sub] = acc[p];
-            }
-        } else {
-            double acc[16];
-#pragma unroll
-            for (int c = 0; c < 16; ++c) acc[c] = 0.0;
-            for (int idx = w; idx < s; idx += 16) {
-                const int I = blk(idx);
-#pragma unroll 2
-                for (int p = 0; p < 4; ++p) {
-                    f4_t v[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        v[u] = *reinterpret_cast<const f4_t*>(
-                            Lb + (int64_t)(I * 64 + 16 * p + sub) * A.ld + J * 64 + 16 * q + 4 * u);
-                    const double x = xs[I * 64 + 16 * p + sub];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            acc[4 * u + e] = fma((double)v[u][e], x, acc[4 * u + e]);
-                }
-            }
-            // column sums: lanes with the same q share columns 16q .. 16q+15
-#pragma unroll
-            for (int c = 0; c < 16; ++c) {
-                acc[c] += __shfl_xor(acc[c], 4, 64);
-                acc[c] += __shfl_xor(acc[c], 8, 64);
-                acc[c] += __shfl_xor(acc[c], 16, 64);
-                acc[c] += __shfl_xor(acc[c], 32, 64);
-            }
-            if (sub == 0) {
-#pragma unroll
-                for (int c = 0; c < 16; ++c) part[w * 64 + 16 * q + c] = acc[c];
-            }
-        }
-        __syncthreads();
-        if (t < 64) {
-            double sum = 0.0;
-            const int nw = s < 16 ? s : 16;  // waves that had a solved block
-            for (int ww = 0; ww < nw; ++ww) sum += part[ww * 64 + t];
-            rj[t] = rb[J * 64 + t] - sum;
-        }
-        __syncthreads();
-        if (t < 256) {  // x_J = inv(L_JJ) rj (FWD) or inv(L_JJ)^T rj (BWD): thread (c, qq)
-            const int c = t >> 2, qq = t & 3;
-            const float* D = Db + (int64_t)J * 4096;
-            double sum = 0.0;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = 16 * qq + e;
-                sum = fma((double)(FWD ? D[c * 64 + m] : D[m * 64 + c]), rj[m], sum);
-            }
-            sum += __shfl_xor(sum, 1, 64);
-            sum += __shfl_xor(sum, 2, 64);
-            if (qq == 0) {
-                xs[J * 64 + c] = sum;
-                ob[J * 64 + c] = sum;
-                if (__builtin_isnan(sum)) bad = 1;
-            }
-        }
-        __syncthreads();
-    }
-    if (t == 0 && bad) live.status[b] = fail_code;
-}
-
-void trsv32_wg_init() {
-    const int mx = (int)(sizeof(double) * (TRF_MAXNP + 16 * 64 + 64));
-    (void)hipFuncSetAttribute((const void*)k_trsv32_wg<true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-    (void)hipFuncSetAttribute((const void*)k_trsv32_wg<false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-}
-
-void launch_trsv32_wg(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
-                      const double* r, double* out, int64_t vstride, Live live, int nchains,
-                      int fail_code, hipStream_t s) {
-    const size_t lds = sizeof(double) * (nb * 64 + 16 * 64 + 64);
-    if (fwd)
-        hipLaunchKernelGGL(k_trsv32_wg<true>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
-                           dstride, r, out, vstride, live, fail_code);
-    else
-        hipLaunchKernelGGL(k_trsv32_wg<false>, dim3(nchains), dim3(1024), lds, s, A, nb, Dinv,
-                           dstride, r, out, vstride, live, fail_code);
-}
-
 bool trsv32_mw_ok(int np) { return np <= TRF_MAXNP; }
 
 // dynamic LDS above the default 64 KiB cap (np up to TRF_MAXNP); apm_create calls it with the
 // context's device current
 void trsv32_mw_init() {
-    trsv32_wg_init();
     const int mx = (int)(sizeof(double) * (TRF_MAXNP + 4 * 64 + 64));
     (void)hipFuncSetAttribute((const void*)k_trsv32_mw<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, mx);

@@ -391,22 +391,6 @@ def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
 
 
 @pytest.mark.parametrize('n', [700, 1100])
-def test_trsv_single_workgroup_matches_multi_workgroup(nat, monkeypatch, n):
-    """The Newton TRSVs by one 1024-thread workgroup per chain (k_trsv32_wg, APM_TRSV_WG=1)
-    against the multi-workgroup solve: the same fp32 factor and fp64 vectors, the sums in another
-    order, absorbed by the fp64 refinement - same iteration counts, modes to 1e-10 of their
-    maximum, estimates to 1e-8 nats."""
-    X, y, thetas, ns = _mixed_case(n=n)
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_TRSV_WG=0)
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_TRSV_WG=1)
-    assert (s0 == 0).all() and (s1 == 0).all()
-    np.testing.assert_array_equal(n1, n0)
-    for b in range(len(thetas)):
-        assert np.abs(f1[b] - f0[b]).max() <= 1e-10 * np.abs(f0[b]).max(), b
-        assert abs(o1[b] - o0[b]) <= 1e-8 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
-
-
-@pytest.mark.parametrize('n', [700, 1100])
 def test_posterior_bottom_fp32_matches_fp64(nat, monkeypatch, n):
     """The posterior factor's bottom block (L_K J) L'^-T in fp32 (default: beside the fp64
     factorisation of J M J on the second stream, APM_POST32=1: after it; postcov.hip) against
