@@ -534,6 +534,36 @@ def ess_block(dist, smp, series, done, burn, elapsed, P):
                           'gelman.diag restatement, max over components (and ranks)'.format(P)}}
 
 
+def stationary_theta_call(smp, a, run_theta_call_s):
+    """One 64-chain theta-call at the long-chain record's chain states (profiles/
+    r*_stationary_thetas.npy: the stationary regime the ESS figure describes), timed live on this
+    rank's device after the timed region (untimed), beside this run's mean theta-call."""
+    import glob
+    from gpdemo import _native
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_stationary_thetas.npy')))
+    if not files or (a.n, a.d, a.n_imp) != (4096, 32, 256):
+        return None
+    th = np.load(files[-1])
+    C = min(a.chains, th.shape[0])
+    if th.shape[1] != smp.P or C < 1:
+        return None
+    idx = np.arange(C)
+    times, nops, st = [], None, None
+    for _ in range(3):  # the first call warms the tile lists of this batch size
+        t0 = time.perf_counter()
+        _, st, nops = smp.ctx.theta_eval(_native.EST_IS, th[:C], smp.ub_u[idx], smp.slot_prop[idx])
+        times.append(time.perf_counter() - t0)
+    return {'source': os.path.relpath(files[-1], REPO), 'chains': int(C),
+            'theta_call_ms': 1e3 * float(np.median(times[1:])),
+            'newton_iterations_mean': float(np.mean(nops - 3)),
+            'newton_iterations_max': int(np.max(nops - 3)),
+            'status_ok': bool((st == 0).all()),
+            'this_run_theta_call_ms_mean': 1e3 * run_theta_call_s,
+            'note': 'untimed; the stationary chains need more Newton iterations per theta-call '
+                    'than this run\'s prior-initialised ones, hence the long-chain record\'s '
+                    'lower transitions/s (ess_long_chain.stationary_transitions_per_s)'}
+
+
 def ess_long_record(value, a):
     """The long-chain ESS record of this workload (SURVEY.md §8d protocol, Analyse
     results.ipynb:138-141: R-hat and ESS on long chains after a warm-up; tools/ess_long.py on one
@@ -772,6 +802,7 @@ def main():
         -(done[~smp.failed].min() if (~smp.failed).any() else 0)))
     ess['sample']['timed_transitions_per_chain_max'] = int(dist.max(done.max()))
     failed = int(dist.sum(int(smp.failed.sum())))
+    stationary = stationary_theta_call(smp, a, wall['theta_call'] / max(1, len(call_ops)))
     ctx.close()  # frees the chains' workspaces before the parity context
 
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
@@ -842,6 +873,7 @@ def main():
     line.update(extra)
     # the PMC numbers (traffic, mfma_busy) come from a committed counter pass: of this build?
     line['pmc_provenance'] = pmc_provenance()
+    line['stationary_theta_call'] = stationary
     line['ess_long_chain'] = lr = ess_long_record(value, a)
     if lr is not None:  # the headline ESS/s from mixed (or, if not yet, the longest) chains
         line['ess_sample']['ess_per_sec_in_run'] = line['ess_per_sec']
