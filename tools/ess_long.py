@@ -88,6 +88,9 @@ def summarise(chains, live, warmup, seg_walls, seg_transitions, cfg):
     tps = ntr / wall if wall > 0 else None
     ept_min = float(ess.min(1).mean() / keep)
     ept_mean = float(ess.mean(1).mean() / keep)
+    # the same per chain over all of its draws (chains that ran ahead in the 'finish' mode)
+    full = [chains[c][warmup:] for c in live]
+    ept_all = float(np.mean([effective_size(x).min() / x.shape[0] for x in full]))
     seg_tps = [t / w if w > 0 else None for t, w in zip(seg_transitions, seg_walls)]
     return {
         'what': 'long-chain ESS / R-hat at BASELINE configs[2] (SURVEY.md §8d protocol), '
@@ -106,6 +109,8 @@ def summarise(chains, live, warmup, seg_walls, seg_transitions, cfg):
         'ess_per_transition_min_component': ept_min,
         'ess_per_transition_mean_component': ept_mean,
         'ess_per_transition_min_component_worst_chain': float(ess.min(1).min() / keep),
+        'ess_per_transition_min_component_all_draws': ept_all,
+        'kept_per_chain_all_draws_mean': float(np.mean([x.shape[0] for x in full])),
         'ess_per_sec_min_component': ept_min * tps if tps else None,
         'ess_per_sec_mean_component': ept_mean * tps if tps else None,
         'rhat_max': float(rhat.max()), 'rhat_median': float(np.median(rhat)),
