@@ -77,13 +77,26 @@ void launch_chol_diag32(MatF A, int k, float* Dinv, int64_t dstride, double* lde
                         int64_t lstride, Live live, int fail_code, int nchains, hipStream_t s);
 void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const float* Dinv,
                          int64_t dstride, Live live, int nchains, hipStream_t s);
+// Bounded in-launch hand-overs of the Newton solve (k_chol_panel_df32, k_trsv32_mw). HIP promises
+// no dispatch order, so a workgroup's logical index is the ticket it draws from a monotonic
+// arrival counter when it starts (a ticket exists only for a workgroup that is running): a
+// dataflow row then waits only on rows that have arrived, and of the TRSV's chains only the one
+// holding the newest ticket can wait on a workgroup that has not. Every wait is bounded by
+// `limit` polls; a bounded exit is counted in *timeouts and fails its chain (the Newton loop
+// reruns it in fp64), so it can cost time but never a value.
+struct SpinCtl {
+    unsigned long long* ticket;    // arrival counter, shared by the launches of one stream
+    unsigned long long base;       // its value before this launch (host-side running total)
+    unsigned long long* timeouts;  // bounded-spin exits (APM_PROF_DF / _TRSV_TIMEOUTS)
+    int limit;                     // polls before a wait gives up
+};
 // tile columns [K, K+ncols) of an outer panel (diagonal tile (K, K) already factored) in one
 // dataflow launch (chol32.hip: per-(chain, row) progress words prog[b * pstride + row], monotonic
-// base per factorisation and panel)
-bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
+// base per factorisation and panel); returns the launch's workgroup count (its tickets), 0 when
+// nothing was launched, -1 for a panel wider than the progress word allows
+long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base,
-                            unsigned long long* timeouts, hipStream_t s);
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s);
 // rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is final (fd.Dinv: its
 // inverses), each row a left-looking walk over the panel's columns with no waits; zrow > 0: row
 // tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)
@@ -123,9 +136,10 @@ void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double
 // first; fp64 r -> out, r kept); needs np <= 8192 (trsv32_mw_ok), else the per-block steps above
 bool trsv32_mw_ok(int np);
 void trsv32_mw_init();  // per device, once the device is current (apm_create)
-void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+// returns the launch's workgroup count (its tickets)
+long launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
-                      int fail_code, hipStream_t s);
+                      int fail_code, SpinCtl sc, hipStream_t s);
 // refinement vector ops (mode 0: out = Ws x; 1: out = Ws Kb - x - Ws Kt; 2: x += out)
 // acceptance of refinement step `step` on the chains with refining[b] != 0 && status[b] == 0:
 // accepted chains leave the mask; with last = true the others get status = fail_code

@@ -108,8 +108,13 @@ struct apm_ctx {
     // in-panel factorisation of the Newton matrix: one dataflow launch per outer panel
     // (k_chol_panel_df32; APM_DF32=0: the launch sequence it replaces)
     bool df32 = true;
-    unsigned long long* dfprog = nullptr;  // per (chain, row tile) progress words
+    // per (chain, row tile) progress words, then [dataflow timeouts][TRSV timeouts][ticket]
+    unsigned long long* dfprog = nullptr;
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
+    // the arrival-ticket counter of the main stream's hand-over kernels (SpinCtl): reset at the
+    // start of every theta-call, ticket_base = the tickets the call's launches have drawn so far
+    unsigned long long ticket_base = 0;
+    int spin_df = 1 << 22, spin_trsv = 1 << 20;  // poll bounds (APM_SPIN_LIMIT: tests only)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
     // previous convergence read; update_flops x live_n instead of x count)
     int live_n = 0;
@@ -354,6 +359,24 @@ void chol_range(apm_ctx* c, MatB M, int k0, int k1, int R, int Cb, int fail_code
 }
 
 // ---- fp32 factorisation of the Newton matrix (chol32.hip), in the memory of the work matrix
+unsigned long long* spin_words(apm_ctx* c) {  // [dataflow timeouts][TRSV timeouts][ticket]
+    return c->dfprog + (size_t)c->max_batch * (c->nb + 1);
+}
+SpinCtl spin_ctl(apm_ctx* c, bool trsv) {
+    unsigned long long* w = spin_words(c);
+    return SpinCtl{w + 2, c->ticket_base, trsv ? w + 1 : w, trsv ? c->spin_trsv : c->spin_df};
+}
+void reset_tickets(apm_ctx* c) {
+    HIPC(hipMemsetAsync(spin_words(c) + 2, 0, sizeof(unsigned long long), c->stream));
+    c->ticket_base = 0;
+}
+void trsv32(apm_ctx* c, bool fwd, MatF F, const float* D, int64_t ds, const double* r,
+            double* out, Live lv, int count) {
+    c->ticket_base += (unsigned long long)launch_trsv32_mw(
+        fwd, F, c->nb, D, ds, r, out, c->v.vstride, lv, count, APM_STATUS_CHOL_B,
+        spin_ctl(c, true), c->stream);
+    check_launch();
+}
 MatF b32_of(apm_ctx* c) {
     return MatF{reinterpret_cast<float*>(c->A.base), c->np, 2 * c->A.cstride};
 }
@@ -414,14 +437,14 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
-            if (!launch_chol_panel_df32(M, K, Kend - K, R,
-                                        FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code},
-                                        lv, count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog,
-                                        c->nb + 1,
-                                        (fact << 16) | ((unsigned long long)(K / c->outer32) << 4),
-                                        c->dfprog + (size_t)c->max_batch * (c->nb + 1), c->stream))
-                throw HipError{"dataflow Newton panel wider than 14 tiles"};
+            const long tickets = launch_chol_panel_df32(
+                M, K, Kend - K, R, FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
+                count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
+                (fact << 16) | ((unsigned long long)(K / c->outer32) << 4), spin_ctl(c, false),
+                c->stream);
+            if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
+            c->ticket_base += (unsigned long long)tickets;
             have_diag = Kend < k1;
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                              fail_code);
@@ -535,8 +558,7 @@ void newton_solve32(apm_ctx* c, int count) {
     const bool mw_trsv = trsv32_mw_ok(np);
     if (mw_trsv) {
         feed_chol_k(c);
-        launch_trsv32_mw(false, F, nb, D, ds, r1, c->v.z, vs, lv, count, APM_STATUS_CHOL_B, s);
-        check_launch();
+        trsv32(c, false, F, D, ds, r1, c->v.z, lv, count);
     } else {
         for (int J = nb - 1; J >= 0; --J) {
             launch_trsv_bwd32(F, J, D, ds, r1, c->v.z, vs, lv, count, s);
@@ -562,11 +584,9 @@ void newton_solve32(apm_ctx* c, int count) {
         check_launch();
         if (mw_trsv) {
             feed_chol_k(c);
-            launch_trsv32_mw(true, F, nb, D, ds, r1, r2, vs, lr, count, APM_STATUS_CHOL_B, s);
-            check_launch();
+            trsv32(c, true, F, D, ds, r1, r2, lr, count);
             feed_chol_k(c);
-            launch_trsv32_mw(false, F, nb, D, ds, r2, r3, vs, lr, count, APM_STATUS_CHOL_B, s);
-            check_launch();
+            trsv32(c, false, F, D, ds, r2, r3, lr, count);
         } else {
             for (int J = 0; J < nb; ++J) {
                 launch_trsv_fwd32(F, J, nb, D, ds, r1, r2, vs, lr, count, s);
@@ -937,6 +957,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     HIPC(hipMemsetD32Async(c->active, 1, count, c->stream));
     HIPC(hipMemsetAsync(c->status, 0, sizeof(int) * count, c->stream));
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
+    reset_tickets(c);
     // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
     const bool ov = est == APM_EST_IS && c->mixed && c->overlap_k;
     // the matrix a factorisation of K starts from (chol(K)'s working copy BL, or PriorMC's A):
@@ -1093,6 +1114,9 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
     if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
+    // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
+    // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
+    if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1165,9 +1189,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, 2 * B);
     c->h3post = c->h3ok + B;
-    // + 1: the count of bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS)
-    c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 1);
-    HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 1)));
+    // + 3: the bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS) and of the
+    // TRSV (APM_PROF_TRSV_TIMEOUTS), the arrival-ticket counter (spin_words)
+    c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 3);
+    HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 3)));
     // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:
     // [i3: 3B int64][ca: B][cb: B][seeds: B][ctrs: B]
     c->d_i3 = dalloc<int64_t>(c, 7 * B);
@@ -1695,8 +1720,8 @@ int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, dou
     try {
         HIPC(hipSetDevice(c->device));
         sync(c);
-        if (kind == APM_PROF_DF_TIMEOUTS) {
-            unsigned long long* d = c->dfprog + (size_t)c->max_batch * (c->nb + 1);
+        if (kind == APM_PROF_DF_TIMEOUTS || kind == APM_PROF_TRSV_TIMEOUTS) {
+            unsigned long long* d = spin_words(c) + (kind == APM_PROF_TRSV_TIMEOUTS ? 1 : 0);
             unsigned long long h = 0;
             HIPC(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost));
             if (total_ms) *total_ms = 0.0;

@@ -330,7 +330,6 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 // progress; a bounded spin marks the chain failed instead of hanging (the Newton loop then reruns
 // it in fp64).
 #define DF_FAILED 15
-#define DF_SPIN (1 << 22)
 #ifndef DF_UNROLLED
 #define DF_UNROLLED true
 #endif
@@ -384,8 +383,7 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          const int* __restrict__ h3ok,
                                                          unsigned long long* prog,
                                                          int64_t pstride,
-                                                         unsigned long long base,
-                                                         unsigned long long* timeouts,
+                                                         unsigned long long base, SpinCtl sc,
                                                          int row0 = 0, int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
@@ -406,8 +404,26 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
         b = (int)(item / rows);
         i = row0 + (int)(item % rows);
     } else {
-        b = (int)(blockIdx.x % nchains);
-        i = K + (int)(blockIdx.x / nchains);
+        // logical index = arrival ticket (SpinCtl): row i waits only on rows k < i of its chain,
+        // i.e. on workgroups that have already arrived - resident or finished, whatever the
+        // dispatch order
+        if (threadIdx.x == 0)
+            seen = __hip_atomic_fetch_add(sc.ticket, 1ull, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) - sc.base;
+        __syncthreads();
+        const unsigned long long lin = seen;
+        __syncthreads();  // (`seen` is reused by the waits)
+        if (lin >= (unsigned long long)(R - K) * nchains) {
+            // tickets out of step with the host's count (a launch that never ran): rows would go
+            // unprocessed, so every chain of the launch fails (fp64 rerun) instead
+            if (threadIdx.x == 0) {
+                for (int c = 0; c < nchains; ++c) live.status[c] = fd.fail_code;
+                atomicAdd(sc.timeouts, 1ull);
+            }
+            return;
+        }
+        b = (int)(lin % nchains);
+        i = K + (int)(lin / nchains);
     }
     const bool pub = !BULK && i < Kend;  // rows of the diagonal block: later rows wait on them
     unsigned long long* pr = prog + b * pstride;
@@ -424,8 +440,8 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
             unsigned long long v =
                 __hip_atomic_load(pr + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int spins = 0; v < need; ++spins) {
-                if (spins > DF_SPIN) {  // counted apart from breakdowns (APM_PROF_DF_TIMEOUTS)
-                    atomicAdd(timeouts, 1ull);
+                if (spins > sc.limit) {  // counted apart from breakdowns (APM_PROF_DF_TIMEOUTS)
+                    atomicAdd(sc.timeouts, 1ull);
                     v = base + DF_FAILED;
                     break;
                 }
@@ -608,18 +624,17 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
     }
 }
 
-bool launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
+long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base,
-                            unsigned long long* timeouts, hipStream_t s) {
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s) {
     // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
     // caller raises) instead of being left unfactored
-    if (ncols > 14) return false;
-    if (ncols < 1 || R - K <= 1) return true;  // (one column: its panel TRSM)
-    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)((long)(R - K) * nchains)), dim3(256),
-                       0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base,
-                       timeouts);
-    return true;
+    if (ncols > 14) return -1;
+    if (ncols < 1 || R - K <= 1) return 0;  // (one column: its panel TRSM)
+    const long grid = (long)(R - K) * nchains;
+    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
+                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc);
+    return grid;
 }
 
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
@@ -628,7 +643,7 @@ void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zro
     if (ncols < 1 || R <= row0) return;
     hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
-                       (int64_t)0, 0ull, nullptr, row0, zrow);
+                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0}, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -1244,11 +1259,15 @@ __global__ __launch_bounds__(256) void k_trsv_bwd32(MatF A, int J, const float* 
 // NaN (no flags, no fences: each value carries its own readiness, and gfx950 agent-scope atomics
 // bypass the XCD-private L2). The contributions of all but the previous step's block are summed
 // before waiting for it, so the critical path per step is one hand-over, one tile and the 64x64
-// inverse product. Polling is bounded: a chain whose solution never appears (a NaN produced by the
-// factor) is marked failed instead of spinning. Waiting only on blocks of the same launch is safe:
-// the G workgroups of a chain need no other kernel to finish to become resident.
+// inverse product. Polling is bounded (SpinCtl.limit polls per element): a chain whose solution
+// never appears (a NaN produced by the factor, or a hand-over that took too long) is marked
+// failed and counted (APM_PROF_TRSV_TIMEOUTS) instead of spinning; the Newton loop reruns it in
+// fp64. Roles come from arrival tickets (SpinCtl): chain b is served by tickets bG .. bG+G-1, so
+// the G roles of every chain but the one holding the newest ticket have all arrived - at most
+// G - 1 workgroups of a launch can wait on one that has not (role g waits on every role, the
+// round-robin step order has no lower-index-only form), and they wait only until any other
+// workgroup on the GPU retires and frees a slot for it.
 #define TRM_G 4         // workgroups per chain
-#define TRM_SPIN (1 << 20)  // polls per element before the chain is declared failed
 __global__ __launch_bounds__(256) void k_nan_fill(double* out, int64_t vstride, int np,
                                                   Live live) {
     const int b = blockIdx.y;
@@ -1261,8 +1280,25 @@ template <bool FWD>
 __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* Dinv,
                                                    int64_t dstride, const double* r, double* out,
                                                    int64_t vstride, Live live, int fail_code,
-                                                   int G) {
-    const int b = blockIdx.x / G, g = blockIdx.x % G;
+                                                   int G, int nchains, SpinCtl sc) {
+    __shared__ int bad;
+    __shared__ unsigned long long tk;
+    if (threadIdx.x == 0) {
+        bad = 0;
+        tk = __hip_atomic_fetch_add(sc.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+             sc.base;
+    }
+    __syncthreads();  // `bad` is read by every poll loop
+    if (tk >= (unsigned long long)nchains * G) {
+        // tickets out of step with the host's count (a launch that never ran): fail every chain
+        // of the launch (fp64 rerun) rather than leave a role unserved
+        if (threadIdx.x == 0) {
+            for (int c = 0; c < nchains; ++c) live.status[c] = fail_code;
+            atomicAdd(sc.timeouts, 1ull);
+        }
+        return;
+    }
+    const int b = (int)(tk / G), g = (int)(tk % G);
     if (!live32(live, b)) return;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row = t >> 2, q = t & 3;  // tile row, 16-column quarter
@@ -1270,9 +1306,6 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
     double* xs = trm_sm;               // np: solution blocks fetched so far (solve order)
     double* red = xs + nb * 64;        // 4 x 64 column-sum partials (BWD)
     double* rj = red + 4 * 64;         // 64: right-hand side of the step
-    __shared__ int bad;
-    if (t == 0) bad = 0;
-    __syncthreads();  // `bad` is read by every poll loop
     const float* Lb = A.base + b * A.cstride;
     const float* Db = Dinv + b * dstride;
     const double* rb = r + b * vstride;
@@ -1284,7 +1317,7 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
             const int I = blk(a + x / 64), o = I * 64 + (x & 63);
             double v = __hip_atomic_load(ob + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int n = 0;
-            while (__builtin_isnan(v) && n < TRM_SPIN && !bad) {
+            while (__builtin_isnan(v) && n < sc.limit && !bad) {
                 __builtin_amdgcn_s_sleep(1);
                 v = __hip_atomic_load(ob + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ++n;
@@ -1409,7 +1442,10 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
         }
     }
     __syncthreads();
-    if (t == 0 && bad) live.status[b] = fail_code;
+    if (t == 0 && bad) {
+        live.status[b] = fail_code;
+        atomicAdd(sc.timeouts, 1ull);
+    }
 }
 
 bool trsv32_mw_ok(int np) { return np <= TRF_MAXNP; }
@@ -1424,9 +1460,9 @@ void trsv32_mw_init() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, mx);
 }
 
-void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
+long launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstride,
                       const double* r, double* out, int64_t vstride, Live live, int nchains,
-                      int fail_code, hipStream_t s) {
+                      int fail_code, SpinCtl sc, hipStream_t s) {
     const size_t lds = sizeof(double) * (nb * 64 + 4 * 64 + 64);
     const int np = nb * 64;
     const int G = TRM_G;
@@ -1434,10 +1470,11 @@ void launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstri
                        np, live);
     if (fwd)
         hipLaunchKernelGGL(k_trsv32_mw<true>, dim3(nchains * G), dim3(256), lds, s, A, nb,
-                           Dinv, dstride, r, out, vstride, live, fail_code, G);
+                           Dinv, dstride, r, out, vstride, live, fail_code, G, nchains, sc);
     else
         hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * G), dim3(256), lds, s, A, nb,
-                           Dinv, dstride, r, out, vstride, live, fail_code, G);
+                           Dinv, dstride, r, out, vstride, live, fail_code, G, nchains, sc);
+    return (long)nchains * G;
 }
 
 void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,

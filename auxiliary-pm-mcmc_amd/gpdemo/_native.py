@@ -20,7 +20,7 @@ APM_SUCCESS, APM_E_INVALID, APM_E_HIP, APM_E_NOMEM = 0, -1, -2, -3
 STATUS_OK, STATUS_CHOL_K, STATUS_CHOL_B, STATUS_CHOL_C, STATUS_MAXITER = 0, 1, 2, 3, 4
 PROF_GRAM, PROF_CHOL_UPDATE, PROF_UGEMM, PROF_CHOL_UPDATE32, PROF_STATS = 0, 1, 2, 3, 4
 PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER, PROF_DF_TIMEOUTS = 5, 6, 7
-PROF_POST32_OUTER, PROF_POST64_RERUNS, PROF_NKINDS = 8, 9, 10
+PROF_POST32_OUTER, PROF_POST64_RERUNS, PROF_TRSV_TIMEOUTS, PROF_NKINDS = 8, 9, 10, 11
 
 
 class NativeUnavailableError(RuntimeError):

@@ -369,8 +369,26 @@ def parity_inputs(n, d, s):
     return thetas, rng.normal(size=(n, s)), rng.normal(size=(n, s))
 
 
+def device_counters(ctx):
+    """The context's bounded-spin exits and precision fallbacks since its last reset (DESIGN.md
+    §3.1, §9): [fp64 Newton reruns, refinement steps, dataflow-panel spin timeouts, TRSV spin
+    timeouts, fp64 posterior-bottom reruns] - a chain that timed out is rerun in fp64 or
+    reported failed, never returned as a wrong value with status 0 (tests/test_gpu_errors.py)."""
+    from gpdemo import _native
+    _, rerun, refine = ctx.prof_read(_native.PROF_STATS, reset=True)
+    _, df_to, _ = ctx.prof_read(_native.PROF_DF_TIMEOUTS, reset=True)
+    _, trsv_to, _ = ctx.prof_read(_native.PROF_TRSV_TIMEOUTS, reset=True)
+    _, post64, _ = ctx.prof_read(_native.PROF_POST64_RERUNS, reset=True)
+    return np.array([rerun, refine, df_to, trsv_to, post64], dtype=np.float64)
+
+
+COUNTER_NAMES = ('newton_fp64_reruns', 'newton_refinement_steps', 'dataflow_spin_timeouts',
+                 'trsv_spin_timeouts', 'posterior_bottom_fp64_reruns')
+
+
 def gpu_parity(X, y, n_imp, thetas, U1, U2, device):
-    """This rank's GPU values: batched theta-call (U1) + cached u-call (U2) at every theta."""
+    """This rank's GPU values: batched theta-call (U1) + cached u-call (U2) at every theta, and
+    the parity context's device counters (device_counters)."""
     from gpdemo import _native
     B = thetas.shape[0]
     ctx = _native.Context(X, y, _native.KERNEL_ARD, 1e-8, n_imp, max_batch=B, n_slots=B,
@@ -381,9 +399,11 @@ def gpu_parity(X, y, n_imp, thetas, U1, U2, device):
         v1, st1, nops = ctx.theta_eval(_native.EST_IS, thetas, [0] * B, list(range(B)))
         v2, st2 = ctx.u_eval(list(range(B)), [1] * B)
         fpost = np.stack([ctx.slot_read(b)[1] for b in range(B)])
+        ctrs = device_counters(ctx)
     finally:
         ctx.close()
-    return v1, v2, nops.astype(np.float64), np.maximum(st1, st2).astype(np.float64), fpost
+    return (v1, v2, nops.astype(np.float64), np.maximum(st1, st2).astype(np.float64), fpost,
+            np.r_[st1, st2].astype(np.float64), ctrs)
 
 
 def reference_fixture(X, y, n, d, s, seed):
@@ -410,11 +430,14 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
     # an exception on one rank must not leave the others waiting in a collective: it is
     # recorded, NaN stands in for the values, and the check fails
     try:
-        g1, g2, gops, gst, gf = gpu_parity(X, y, a.n_imp, thetas, U1, U2, rank_device(dist))
+        g1, g2, gops, gst, gf, gst12, gctr = gpu_parity(X, y, a.n_imp, thetas, U1, U2,
+                                                        rank_device(dist))
     except Exception as e:  # noqa: BLE001
         errors.append('rank {0} GPU: {1!r}'.format(dist.rank, e))
         g1 = g2 = gops = np.full(B, np.nan)
         gst = np.full(B, -1.0)
+        gst12 = np.full(2 * B, -1.0)
+        gctr = np.full(len(COUNTER_NAMES), np.nan)
         gf = np.full((B, n), np.nan)
     orc_vals = np.zeros((B, 3))
     orc_f = np.zeros((B, n))
@@ -442,9 +465,23 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
     orc_f = dist.broadcast(orc_f)
     fscale = np.abs(orc_f).max(1)
     mine = np.concatenate([g1 - orc_vals[:, 0], g2 - orc_vals[:, 1], gops - orc_vals[:, 2], gst,
-                           np.abs(gf - orc_f).max(1) / fscale, g1, g2])
-    allr = dist.all_gather(mine)  # (world, 7B)
+                           np.abs(gf - orc_f).max(1) / fscale, g1, g2, gst12, gctr])
+    allr = dist.all_gather(mine)  # (world, 9B + counters)
     d1, d2, dops, st, frel = (allr[:, k * B:(k + 1) * B] for k in range(5))
+    # per rank: every value, status and device counter of its own parity context, so that a
+    # failure names the rank, the theta and the path (round-4 verdict: an intermittent 2-rank
+    # failure whose block was lost to a truncated log)
+    per_rank = []
+    for r in range(allr.shape[0]):
+        row = allr[r]
+        ctr = row[9 * B:]
+        per_rank.append({
+            'rank': r, 'd_theta_call': row[:B].tolist(), 'd_u_call': row[B:2 * B].tolist(),
+            'd_n_cubic_ops': row[2 * B:3 * B].tolist(), 'f_post_max_rel': row[4 * B:5 * B].tolist(),
+            'status_theta_call': row[7 * B:8 * B].astype(int).tolist(),
+            'status_u_call': row[8 * B:9 * B].astype(int).tolist(),
+            'device_counters': {k: (None if np.isnan(v) else int(v))
+                                for k, v in zip(COUNTER_NAMES, ctr)}})
     out = {'thetas': ['theta* (log sigma 0, log tau_k log sqrt(D))',
                       'long length-scale (log sigma 1, log tau_k log sqrt(D) + 2)'],
            'draws': 'U1, U2 = first two (N, N_imp) normal draws of RandomState({0}); theta-call '
@@ -459,7 +496,8 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
            'tol': {'abs_nats': PARITY_TOL_NATS, 'f_post_rel': PARITY_FPOST_REL},
            'oracle': {'theta_call': orc_vals[:, 0].tolist(), 'u_call': orc_vals[:, 1].tolist(),
                       'n_cubic_ops': orc_vals[:, 2].astype(int).tolist(),
-                      'seconds': t_orc if dist.rank == 0 else None}}
+                      'seconds': t_orc if dist.rank == 0 else None},
+           'per_rank': per_rank}
     n_err = dist.sum(len(errors))
     if errors:
         out['errors'] = errors
@@ -534,42 +572,36 @@ def ess_block(dist, smp, series, done, burn, elapsed, P):
                           'gelman.diag restatement, max over components (and ranks)'.format(P)}}
 
 
-def stationary_theta_call(smp, a, run_theta_call_s):
-    """One 64-chain theta-call at the long-chain record's chain states (profiles/
-    r*_stationary_thetas.npy: the stationary regime the ESS figure describes), timed live on this
-    rank's device after the timed region (untimed), beside this run's mean theta-call."""
+STATIONARY_DATA_SEED = 20151009  # the long-chain record's data (tools/ess_long.py)
+
+
+def stationary_states(a, P):
+    """Start states of the headline run: the long-chain record's chain states (profiles/
+    r*_stationary_thetas.npy: 64 chains of this workload after 9000 transitions each, where the
+    posterior puts them - log sigma ~3.5, 7-8 Newton iterations per theta-call), so that the timed
+    transitions are the stationary ones that a whole chain is made of (the reference times whole
+    10 000-transition chains, E-SS+RD-SS.ipynb:203-205). Chain c starts from state c mod 64; u is
+    drawn fresh. (None, why) for another workload: the run then starts from prior draws."""
     import glob
-    from gpdemo import _native
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_stationary_thetas.npy')))
-    if not files or (a.n, a.d, a.n_imp) != (4096, 32, 256):
-        return None
-    th = np.load(files[-1])
-    C = min(a.chains, th.shape[0])
-    if th.shape[1] != smp.P or C < 1:
-        return None
-    idx = np.arange(C)
-    times, nops, st = [], None, None
-    for _ in range(3):  # the first call warms the tile lists of this batch size
-        t0 = time.perf_counter()
-        _, st, nops = smp.ctx.theta_eval(_native.EST_IS, th[:C], smp.ub_u[idx], smp.slot_prop[idx])
-        times.append(time.perf_counter() - t0)
-    return {'source': os.path.relpath(files[-1], REPO), 'chains': int(C),
-            'theta_call_ms': 1e3 * float(np.median(times[1:])),
-            'newton_iterations_mean': float(np.mean(nops - 3)),
-            'newton_iterations_max': int(np.max(nops - 3)),
-            'status_ok': bool((st == 0).all()),
-            'this_run_theta_call_ms_mean': 1e3 * run_theta_call_s,
-            'note': 'untimed; the stationary chains need more Newton iterations per theta-call '
-                    'than this run\'s prior-initialised ones, hence the long-chain record\'s '
-                    'lower transitions/s (ess_long_chain.stationary_transitions_per_s)'}
+    if not files:
+        return None, 'no stationary-state record'
+    if (a.n, a.d, a.n_imp, a.seed) != (4096, 32, 256, STATIONARY_DATA_SEED):
+        return None, 'the record belongs to another workload'
+    th = np.load(files[-1], allow_pickle=False)
+    if th.ndim != 2 or th.shape[1] != P:
+        return None, 'record shape {0} does not fit theta of length {1}'.format(th.shape, P)
+    return th[np.arange(a.chains) % th.shape[0]].astype(np.float64), \
+        os.path.relpath(files[-1], REPO)
 
 
 def ess_long_record(value, a):
     """The long-chain ESS record of this workload (SURVEY.md §8d protocol, Analyse
     results.ipynb:138-141: R-hat and ESS on long chains after a warm-up; tools/ess_long.py on one
     MI355X -> the newest profiles/r*_ess_long.json): its ESS per transition (min and mean over the
-    theta components) x this run's transitions/s. This is the headline ESS/s: the in-run figure
-    rests on ~100-transition segments whose R-hat shows the chains have not mixed there."""
+    theta components) x `value`, this run's driver-timed transitions/s from the record's own
+    stationary states (ess_per_sec_estimate: the headline), beside the record's own sampling
+    rate (ess_per_sec_record, a builder-run number)."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_ess_long.json')))
     if not files:
@@ -591,8 +623,8 @@ def ess_long_record(value, a):
             'stationary_transitions_per_s': tps_st,
             'stationary_library_sha16': lib.get('sha16'),
             'stationary_posterior_mean_log_sigma': r.get('posterior_mean_log_sigma'),
-            'ess_per_sec_stationary': ept * tps_st if tps_st else None,
-            'ess_mean_per_sec_stationary': eptm * tps_st if tps_st and eptm is not None else None,
+            'ess_per_sec_record': ept * tps_st if tps_st else None,
+            'ess_mean_per_sec_record': eptm * tps_st if tps_st and eptm is not None else None,
             'ess_per_sec_estimate': ept * value,
             'ess_mean_per_sec_estimate': eptm * value if eptm is not None else None,
             'rhat_max': r['rhat_max'], 'rhat_median': r.get('rhat_median'),
@@ -602,32 +634,26 @@ def ess_long_record(value, a):
             'chains': cfg.get('chains'),
             'warmup_discarded': r.get('warmup_discarded', cfg.get('warmup_discarded')),
             'kept_per_chain': r.get('kept_per_chain', cfg.get('kept_per_chain')),
-            'note': 'ESS per transition from the long-chain record x the record\'s own '
-                    'stationary transitions/s (the headline ess_per_sec) or x this run\'s '
-                    'transitions/s (ess_per_sec_estimate: prior-initialised chains, fewer Newton '
-                    'iterations per theta-call than at stationarity)'}
+            'note': 'ESS per transition from the long-chain record x this run\'s driver-timed '
+                    'transitions/s from the record\'s stationary states (ess_per_sec_estimate, '
+                    'the headline ess_per_sec) or x the record\'s own sampling rate '
+                    '(ess_per_sec_record)'}
 
 
-def main():
-    a = parse()
-    dist = Dist()
-    if a.gpus != dist.world:
-        raise SystemExit('bench.py: --gpus {0} but WORLD_SIZE={1}; launch N>1 as `python -m '
-                         'torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr '
-                         '127.0.0.1 --master-port P bench.py --gpus N`'.format(a.gpus, dist.world))
+def run_chains(a, dist, dev, X, y, theta_init, measure):
+    """One batched-chain run of the benchmark workload on this rank's device: `--warmup`
+    untimed transitions per chain, then the timed region (every chain completes >= `--steps`
+    transitions under the asynchronous schedule; chains that are ahead keep working; a final
+    partial transition is not counted). measure: the roofline HIP-event timing and the
+    rocprofv3 window markers bracket the timed region. Returns the sampler (context open) and
+    the run's record."""
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
     from gpdemo import _native
-    from gpdemo.utils import synthetic_gp_data
-
-    dev = rank_device(dist)
-    _SYNC_DEVICE[0] = dev
-    X, y = synthetic_gp_data(a.n, a.d, a.seed)
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
     smp = BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
         seed=chain_seed(a.seed, dist.rank), device=dev)
-    P = smp.P
-    smp.initialise()
+    smp.initialise(theta_init)
     series = [[] for _ in range(a.chains)]  # every transition of each chain (ESS)
     if a.schedule == 'async':
         if a.warmup:
@@ -643,11 +669,12 @@ def main():
     ctx = smp.ctx
     for k in range(_native.PROF_NKINDS):
         ctx.prof_read(k, reset=True)
-    # roofline level: one HIP-event pair per Gram, L.U and rank-512 update launch (the in-panel
-    # update launches are not bracketed: their events cost ~2 % of the theta-call)
-    ctx.prof_enable(1)
+    if measure:
+        # roofline level: one HIP-event pair per Gram, L.U and rank-512 update launch (the
+        # in-panel update launches are not bracketed: their events cost ~2 % of the theta-call)
+        ctx.prof_enable(1)
     device_sync()  # first torch touch outside the timed region
-    mark = lambda: ctx.prof_marker(1)  # noqa: E731  timed-region bracket (tools/prof_window.py)
+    mark = (lambda: ctx.prof_marker(1)) if measure else None  # window bracket (prof_window.py)
     th0, u0 = smp.n_theta_calls, smp.n_u_calls
     smp.call_ops = []
     for h in ctx.batch_hist.values():
@@ -656,9 +683,6 @@ def main():
         smp.wall[k] = 0.
     res = {}
     if a.schedule == 'async':
-        # every chain completes >= K transitions; chains that are ahead keep working until the
-        # slowest has K (every theta-call carries the full batch); all completed transitions
-        # count, a final partial transition of a chain is discarded
         def body():
             res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
         elapsed = timed_region(dist, body, 1, mark)
@@ -672,18 +696,46 @@ def main():
                 series[c].append(th[c].copy())
         elapsed = timed_region(dist, one_step, a.steps, mark)
         done = np.where(smp.failed, 0, a.steps)
-    ctx.prof_marker(2)
-    ctx.prof_enable(False)
+    if measure:
+        ctx.prof_marker(2)
+        ctx.prof_enable(False)
     done = np.where(smp.failed, 0, done)
     local_tr = int(done.sum())
-    local_elapsed = elapsed
     transitions = dist.sum(local_tr)
-    value = transitions / elapsed
-    n_th = (smp.n_theta_calls - th0) / max(1, local_tr)
-    n_u = (smp.n_u_calls - u0) / max(1, local_tr)
     call_ops = list(smp.call_ops)
-    wall = dict(smp.wall)
-    batch_hist = {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()}
+    rec = {'elapsed': elapsed, 'done': done, 'local_tr': local_tr, 'transitions': transitions,
+           'value': transitions / elapsed, 'series': series,
+           'n_th': (smp.n_theta_calls - th0) / max(1, local_tr),
+           'n_u': (smp.n_u_calls - u0) / max(1, local_tr),
+           'call_ops': call_ops, 'wall': dict(smp.wall),
+           'batch_hist': {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()},
+           'theta_call_ms_mean': 1e3 * smp.wall['theta_call'] / max(1, len(call_ops))}
+    return smp, rec
+
+
+def main():
+    a = parse()
+    dist = Dist()
+    if a.gpus != dist.world:
+        raise SystemExit('bench.py: --gpus {0} but WORLD_SIZE={1}; launch N>1 as `python -m '
+                         'torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr '
+                         '127.0.0.1 --master-port P bench.py --gpus N`'.format(a.gpus, dist.world))
+    from gpdemo import _native
+    from gpdemo.utils import synthetic_gp_data
+
+    dev = rank_device(dist)
+    _SYNC_DEVICE[0] = dev
+    X, y = synthetic_gp_data(a.n, a.d, a.seed)
+    P = a.d + 1
+    # headline run: the chains start from the long-chain record's stationary states (the regime
+    # a whole chain is made of); where no record fits the workload, from prior draws
+    th_stat, stat_src = stationary_states(a, P)
+    smp, run = run_chains(a, dist, dev, X, y, th_stat, measure=True)
+    ctx = smp.ctx
+    elapsed, done, local_tr = run['elapsed'], run['done'], run['local_tr']
+    transitions, value = run['transitions'], run['value']
+    n_th, n_u, call_ops, wall = run['n_th'], run['n_u'], run['call_ops'], run['wall']
+    series = run['series']
 
     prof = {}
     for k, name in ((_native.PROF_GRAM, 'gram'), (_native.PROF_CHOL_UPDATE_OUTER, 'chol_update'),
@@ -692,9 +744,7 @@ def main():
                     (_native.PROF_POST32_OUTER, 'post32')):
         prof[name] = ctx.prof_read(k, reset=False)
     ctx.prof_read(0, reset=True)
-    _, n_rerun, n_refine = ctx.prof_read(_native.PROF_STATS, reset=True)
-    _, n_post64, _ = ctx.prof_read(_native.PROF_POST64_RERUNS, reset=True)
-    _, n_df_timeouts, _ = ctx.prof_read(_native.PROF_DF_TIMEOUTS, reset=True)
+    n_rerun, n_refine, n_df_timeouts, n_trsv_timeouts, n_post64 = device_counters(ctx)
 
     def mfma_roofline(name, kernel, peak, shorts, kind):
         ms, cnt, flops = prof[name]
@@ -802,8 +852,25 @@ def main():
         -(done[~smp.failed].min() if (~smp.failed).any() else 0)))
     ess['sample']['timed_transitions_per_chain_max'] = int(dist.max(done.max()))
     failed = int(dist.sum(int(smp.failed.sum())))
-    stationary = stationary_theta_call(smp, a, wall['theta_call'] / max(1, len(call_ops)))
-    ctx.close()  # frees the chains' workspaces before the parity context
+    local_failed = int(smp.failed.sum())
+    ctx.close()  # frees the chains' workspaces before the next context
+
+    # the same workload from prior draws (the reference notebooks' chain start,
+    # E-SS+RD-SS.ipynb:198-201): its first transitions need ~4 Newton iterations per theta-call
+    # against 7-8 at stationarity, so it runs faster than the chains a long run is made of
+    prior_init = None
+    if th_stat is not None:
+        smp2, run2 = run_chains(a, dist, dev, X, y, None, measure=False)
+        prior_init = {'value': run2['value'], 'transitions_timed': int(run2['transitions']),
+                      'ms_per_step': 1e3 * run2['elapsed'] / a.steps,
+                      'theta_calls_per_transition': run2['n_th'],
+                      'u_calls_per_transition': run2['n_u'],
+                      'theta_call_ms_mean': run2['theta_call_ms_mean'],
+                      'cubic_ops_per_theta_call_mean_of_batch_max':
+                          float(np.mean([m for m, _ in run2['call_ops']]))
+                          if run2['call_ops'] else None,
+                      'failed_chains': int(dist.sum(int(smp2.failed.sum())))}
+        smp2.ctx.close()
 
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     cpu, first = None, None
@@ -817,13 +884,18 @@ def main():
             cpu, first = {'error': repr(e)}, None
     parity = parity_check(dist, X, y, a, thetas_par, U1, U2, first) if a.parity else None
 
-    # per-rank record: device, chains, transitions, elapsed (8 distinct devices, even load)
+    # per-rank record: device, chains, transitions, elapsed, failures and the device counters of
+    # the timed run (8 distinct devices, even load, no silent spin exits)
     mine = np.array([float(dist.rank), float(dev), float(a.chains), float(local_tr),
-                     float(local_elapsed), float(int(smp.failed.sum()))])
+                     float(elapsed), float(local_failed), n_rerun, n_df_timeouts,
+                     n_trsv_timeouts, n_post64])
     ranks = [{'rank': int(r[0]), 'device': int(r[1]), 'chains': int(r[2]),
               'transitions': int(r[3]), 'elapsed_s': r[4], 'failed_chains': int(r[5]),
-              'transitions_per_s': r[3] / r[4]} for r in dist.all_gather(mine)]
+              'transitions_per_s': r[3] / r[4], 'newton_fp64_reruns': int(r[6]),
+              'dataflow_spin_timeouts': int(r[7]), 'trsv_spin_timeouts': int(r[8]),
+              'posterior_bottom_fp64_reruns': int(r[9])} for r in dist.all_gather(mine)]
 
+    stationary = th_stat is not None
     line = {
         'metric': METRIC, 'value': value, 'unit': 'transitions/s (all chains, all GPUs)',
         'n_gpus': dist.world, 'steps': a.steps, 'warmup': a.warmup,
@@ -847,48 +919,53 @@ def main():
                    'n_data': a.n, 'n_features': a.d, 'n_imp': a.n_imp, 'n_theta': P,
                    'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
-                   .format(dist.world)},
+                   .format(dist.world),
+                   'chain_start': ('stationary: the long-chain record\'s chain states ({0}), '
+                                   'fresh u, then --warmup transitions'.format(stat_src)
+                                   if stationary else
+                                   'prior draws (E-SS+RD-SS.ipynb:198-201): {0}'.format(stat_src))},
+        'value_prior_init': prior_init,
         'ess_per_sec': ess['ess_per_sec'], 'ess_mean_per_sec': ess['ess_mean_per_sec'],
-        'ess_per_sec_source': 'in-run sample (see ess_sample; replaced by the long-chain record '
-                              'when one exists)',
+        'ess_per_sec_source': 'in-run sample of this run\'s chains (ess_sample)',
+        'ess_per_sec_in_run': ess['ess_per_sec'], 'ess_mean_per_sec_in_run': ess['ess_mean_per_sec'],
         'rhat': ess['rhat'], 'ess_sample': ess['sample'],
         'parity': parity,
         'schedule': a.schedule, 'transitions_timed': int(transitions),
         'theta_calls_per_transition': n_th, 'u_calls_per_transition': n_u,
+        'theta_call_ms_mean': run['theta_call_ms_mean'],
         'failed_chains': failed,
         'newton_refinement_steps': int(dist.sum(n_refine)),
         'newton_fp64_reruns': int(dist.sum(n_rerun)),
         'posterior_bottom_fp64_reruns': int(dist.sum(n_post64)),
         'newton_dataflow_spin_timeouts': int(dist.sum(n_df_timeouts)),
+        'newton_trsv_spin_timeouts': int(dist.sum(n_trsv_timeouts)),
         'cubic_ops_per_theta_call': {
             'mean_of_batch_max': float(np.mean([m for m, _ in call_ops])) if call_ops else None,
             'mean_of_batch_mean': float(np.mean([v for _, v in call_ops])) if call_ops else None,
             'note': 'IS: Newton iterations + 3 (estimators.py:217); a batched call lasts as long '
                     'as its slowest chain'},
         'wall_split_s': dict(wall, host_sampler=elapsed - sum(wall.values())),
-        'calls_by_batch_size': batch_hist,
+        'calls_by_batch_size': run['batch_hist'],
         'ranks': ranks,
         'roofline': roofline, 'cpu_baseline': cpu,
     }
     line.update(extra)
     # the PMC numbers (traffic, mfma_busy) come from a committed counter pass: of this build?
     line['pmc_provenance'] = pmc_provenance()
-    line['stationary_theta_call'] = stationary
     line['ess_long_chain'] = lr = ess_long_record(value, a)
-    if lr is not None:  # the headline ESS/s from mixed (or, if not yet, the longest) chains
-        line['ess_sample']['ess_per_sec_in_run'] = line['ess_per_sec']
-        line['ess_sample']['ess_mean_per_sec_in_run'] = line['ess_mean_per_sec']
-        st = lr['ess_per_sec_stationary'] is not None
-        line['ess_per_sec'] = lr['ess_per_sec_stationary'] if st else lr['ess_per_sec_estimate']
-        line['ess_mean_per_sec'] = (lr['ess_mean_per_sec_stationary'] if st
-                                    else lr['ess_mean_per_sec_estimate'])
+    if lr is not None and stationary:
+        # the headline ESS/s: the long-chain record's ESS per transition (its chains have run
+        # 22 000 transitions; this run's ~150-transition series cannot see the slow modes) x
+        # THIS run's driver-timed stationary transitions/s
+        line['ess_per_sec'] = lr['ess_per_sec_estimate']
+        line['ess_mean_per_sec'] = lr['ess_mean_per_sec_estimate']
         line['ess_per_sec_source'] = (
-            'long-chain record {0}: ESS per transition (min over theta components) x {1}; R-hat '
-            'max {2:.3f} ({3})'.format(
-                lr['source'], 'the record\'s stationary transitions/s ({0:.1f})'.format(
-                    lr['stationary_transitions_per_s']) if st else 'this run\'s transitions/s',
-                lr['rhat_max'],
-                'converged' if lr['converged_rhat_below_1p1'] else 'NOT converged: R-hat > 1.1'))
+            'long-chain record {0}: ESS per transition (min over theta components, {1:.5f}) x '
+            'this run\'s driver-timed transitions/s from the record\'s stationary states '
+            '(value, {2:.1f}); R-hat max {3:.3f} ({4}); the in-run figure is ess_per_sec_in_run'
+            .format(lr['source'], lr['ess_per_transition_min_component'], value, lr['rhat_max'],
+                    'converged' if lr['converged_rhat_below_1p1'] else
+                    'NOT converged: R-hat > 1.1'))
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     ok = parity is None or parity['pass']
@@ -896,7 +973,8 @@ def main():
     del _native
     if not ok:
         if dist.rank == 0:
-            print('bench.py: PARITY FAILED (see the "parity" block)', file=sys.stderr, flush=True)
+            print('bench.py: PARITY FAILED; parity block: ' + json.dumps(parity), file=sys.stderr,
+                  flush=True)
         sys.exit(3)
 
 

@@ -138,7 +138,10 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
                                    bottom block in fp32 (postcov.hip, APM_POST32) */
 #define APM_PROF_POST64_RERUNS 9 /* not a kernel: launches = chains whose posterior bottom block was
                                     recomputed in fp64 (trace of C above the fp32 bound) */
-#define APM_PROF_NKINDS 10
+#define APM_PROF_TRSV_TIMEOUTS 10 /* not a kernel: launches = bounded-spin timeouts of the Newton
+                                    solves' multi-workgroup TRSV (each fails its chain, which the
+                                    Newton loop reruns in fp64) */
+#define APM_PROF_NKINDS 11
 /* on = 0 off; 1 the roofline kinds (GRAM, UGEMM and the two *_OUTER kinds: one event pair per
  * launch of those kernels only, so that the timing adds little to a timed region); 2 every kind
  * (CHOL_UPDATE / CHOL_UPDATE32 add an event pair around every in-panel update launch) */

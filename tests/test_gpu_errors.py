@@ -129,3 +129,50 @@ def test_invalid_covariance_deviation_pinned(nat, name):
     r = orc.is_estimate_reformulated(y, st, ns)
     assert np.isfinite(v)
     assert abs(v - r) <= 5e-4, (v, r)
+
+
+def test_forced_spin_timeouts_never_return_wrong_values(nat, monkeypatch):
+    """The Newton solve's in-launch hand-overs (the dataflow panel k_chol_panel_df32, the
+    multi-workgroup TRSV k_trsv32_mw) wait with bounded spins (chol32.hip SpinCtl). With the
+    bound forced to one poll (APM_SPIN_LIMIT=1, read at context creation) the waits time out:
+    every exit must be counted and must fail its chain, which the Newton loop reruns in fp64 -
+    so each chain comes back with status 0 and the value of an undisturbed context (within the
+    5e-4-nat estimator tolerance, n_cubic_ops equal), or reports a failure; never a wrong value
+    with status 0 (round-4 verdict: an intermittent 2-rank parity failure)."""
+    from gpdemo.utils import synthetic_gp_data
+    n, d, s, B = 700, 8, 32, 6
+    X, y = synthetic_gp_data(n, d, 11)
+    base = np.log(np.sqrt(d))
+    th = np.stack([np.r_[0.3 * k - 0.6, np.full(d, base + 0.2 * (k % 3))] for k in range(B)])
+    rng = np.random.RandomState(4)
+    U1, U2 = rng.normal(size=(n, s)), rng.normal(size=(n, s))
+
+    def run():
+        ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, s, max_batch=B, n_slots=B, n_ubufs=2)
+        try:
+            for k in range(nat.PROF_NKINDS):
+                ctx.prof_read(k, reset=True)
+            ctx.u_upload(0, U1)
+            ctx.u_upload(1, U2)
+            v1, st1, nops = ctx.theta_eval(nat.EST_IS, th, [0] * B, list(range(B)))
+            v2, st2 = ctx.u_eval(list(range(B)), [1] * B)
+            ctr = [ctx.prof_read(k)[1] for k in (nat.PROF_STATS, nat.PROF_DF_TIMEOUTS,
+                                                 nat.PROF_TRSV_TIMEOUTS)]
+        finally:
+            ctx.close()
+        return v1, v2, st1, st2, nops, ctr
+
+    r1, r2, rs1, rs2, rops, rctr = run()
+    assert (rs1 == 0).all() and (rs2 == 0).all()
+    assert rctr[1] == 0 and rctr[2] == 0  # an undisturbed context: no spin exits
+    monkeypatch.setenv('APM_SPIN_LIMIT', '1')
+    v1, v2, st1, st2, nops, ctr = run()
+    reruns, df_to, trsv_to = ctr
+    assert df_to + trsv_to > 0, 'the forced bound produced no timeout: the path was not exercised'
+    assert reruns > 0  # every timed-out chain went to the fp64 rerun
+    ok = (st1 == 0) & (st2 == 0)
+    # a chain either failed visibly or carries the undisturbed value
+    assert ok.all(), (st1, st2)  # (the fp64 rerun has no spin-waits, so none should fail)
+    np.testing.assert_array_equal(nops[ok], rops[ok])
+    assert np.abs(v1[ok] - r1[ok]).max() <= 5e-4, (v1, r1)
+    assert np.abs(v2[ok] - r2[ok]).max() <= 5e-4, (v2, r2)
