@@ -113,6 +113,9 @@ class _BatchedChains(object):
         # accepted elliptical-slice move — u is a deterministic function of these
         self.u_init_ctr = np.zeros(C, dtype=np.uint64)
         self.u_log = [[] for _ in range(C)]
+        # set once a checkpoint has carried u itself (checkpoint(store_u=True)): the history
+        # then starts at that snapshot, so every later checkpoint carries u too
+        self.u_snapshot = False
         self.n_reject_u = np.zeros(C, dtype=np.int64)  # Metropolis independence u-updates
 
     # ------------------------------------------------------------------ helpers
@@ -161,18 +164,29 @@ class _BatchedChains(object):
         self.theta = self.prior_draw() if theta_init is None else np.array(theta_init, float)
         self.u_init_ctr = self.dev_ctr.copy()
         self.u_log = [[] for _ in range(self.n_chains)]
+        self.u_snapshot = False
         self._normals(idx, self.ub_u)
         self.log_f, self.lp_cur = self._theta_eval(idx, self.theta, self.slot_cur[idx])
         return self.theta.copy()
 
     # ------------------------------------------------------------------ checkpoint / resume
-    def checkpoint(self):
+    def checkpoint(self, store_u=False):
         """Chain state at a transition boundary as a dict of numpy arrays (``numpy.savez``-able,
-        no pickles): theta, log f, log prior, failure flags, device counters, each chain's
-        RandomState (MT19937 key and position, cached Gaussian) and the u history. u itself
-        (N x N_imp fp64 per chain) is not stored: ``restore`` rebuilds it on the device from
-        the history with the same kernels, bit for bit."""
+        no pickles): theta, log f, log prior, failure flags, rejection counts, device counters,
+        each chain's RandomState (MT19937 key and position, cached Gaussian) and the u history.
+        By default u itself (N x N_imp fp64 per chain) is not stored: ``restore`` rebuilds it on
+        the device from the history with the same kernels, bit for bit - a replay that grows
+        with the chain. ``store_u=True`` downloads u instead (fp64, exact: the device's fp32
+        mirror is the rounding of those values, so an upload restores both bit for bit) and
+        restarts the history at this snapshot, so restore time and u-log size stop growing;
+        every later checkpoint then carries u as well."""
         C = self.n_chains
+        if store_u or self.u_snapshot:
+            u = np.zeros((C, self.ctx.n, self.n_imp))
+            for c in np.flatnonzero(~self.failed):
+                u[c] = self.ctx.u_download(self.ub_u[c])
+            self.u_log = [[] for _ in range(C)]
+            self.u_snapshot = True
         keys = np.empty((C, 624), dtype=np.uint32)
         pos = np.empty(C, dtype=np.int64)
         has_g = np.empty(C, dtype=np.int64)
@@ -184,12 +198,17 @@ class _BatchedChains(object):
         flat = [r for l in self.u_log for r in l]
         ulog_ctr = np.array([r[0] for r in flat], dtype=np.uint64)
         ulog_cs = np.array([[r[1], r[2]] for r in flat], dtype=np.float64).reshape(-1, 2)
-        return dict(theta=self.theta.copy(), log_f=self.log_f.copy(), lp_cur=self.lp_cur.copy(),
-                    failed=self.failed.copy(), fail_status=self.fail_status.copy(),
-                    dev_seeds=self.dev_seeds.copy(), dev_ctr=self.dev_ctr.copy(),
-                    rng_key=keys, rng_pos=pos, rng_has_gauss=has_g, rng_gauss=gauss,
-                    u_init_ctr=self.u_init_ctr.copy(), ulog_n=n_log, ulog_ctr=ulog_ctr,
-                    ulog_cs=ulog_cs)
+        ck = dict(theta=self.theta.copy(), log_f=self.log_f.copy(), lp_cur=self.lp_cur.copy(),
+                  failed=self.failed.copy(), fail_status=self.fail_status.copy(),
+                  dev_seeds=self.dev_seeds.copy(), dev_ctr=self.dev_ctr.copy(),
+                  rng_key=keys, rng_pos=pos, rng_has_gauss=has_g, rng_gauss=gauss,
+                  u_init_ctr=self.u_init_ctr.copy(), ulog_n=n_log, ulog_ctr=ulog_ctr,
+                  ulog_cs=ulog_cs, n_reject_u=self.n_reject_u.copy())
+        if hasattr(self, 'n_reject'):  # the MH twins' theta rejections
+            ck['n_reject'] = np.asarray(self.n_reject).copy()
+        if self.u_snapshot:
+            ck['u'] = u
+        return ck
 
     def restore(self, ck):
         """Resume from ``checkpoint()`` output (same X, y, chains and seed): host state back,
@@ -213,8 +232,17 @@ class _BatchedChains(object):
         self.u_log = [[(np.uint64(ck['ulog_ctr'][i]), float(ck['ulog_cs'][i, 0]),
                         float(ck['ulog_cs'][i, 1])) for i in range(offs[c], offs[c + 1])]
                       for c in range(C)]
+        if 'n_reject_u' in ck:
+            self.n_reject_u = np.array(ck['n_reject_u'], dtype=np.int64)
+        if 'n_reject' in ck and hasattr(self, 'n_reject'):
+            self.n_reject = np.array(ck['n_reject'], dtype=np.int64)
         idx = np.arange(C)
-        self.ctx.u_normal(self.ub_u[idx], self.dev_seeds[idx], self.u_init_ctr[idx])
+        self.u_snapshot = 'u' in ck
+        if self.u_snapshot:  # u itself (checkpoint(store_u=True)); the history starts there
+            for c in idx:
+                self.ctx.u_upload(self.ub_u[c], np.asarray(ck['u'][c], dtype=np.float64))
+        else:
+            self.ctx.u_normal(self.ub_u[idx], self.dev_seeds[idx], self.u_init_ctr[idx])
         for k in range(int(n_log.max()) if C else 0):
             sel = np.flatnonzero(n_log > k)
             rec = [self.u_log[c][k] for c in sel]
@@ -654,14 +682,17 @@ class _BatchedMHMixin(object):
         return self.n_reject.copy()
 
     def adaptive_run(self, theta_init, batch_size, n_batch, low_acc_thr, upp_acc_thr,
-                     adapt_factor_func, reject_count_index=None):
+                     adapt_factor_func, reject_count_index=-1):
         """BaseAdaptiveMHSampler.adaptive_run (samplers.py:14-156) for every chain: each batch
         restarts get_samples from the previous batch's last state (a fresh estimate there, as
         the reference's get_samples does) and each chain's scales are divided / multiplied by
         adapt_factor_func(b, n_batch) when its batch accept rate is below / above the
         thresholds. Where get_samples returns several rejection counts (MI + MH: u and theta),
-        ``reject_count_index`` picks the one the scales drive (samplers.py:143-144). Returns
-        (thetas (C, n_batch*batch_size, P), scales (C, n_batch, P), accept_rates (C, n_batch))."""
+        ``reject_count_index`` picks the one the scales drive; as in the reference
+        (samplers.py:70, 143-144) it defaults to -1, the last count (the theta step), and a falsy
+        index (0, None) leaves the counts unpicked - which the reference then fails on; here that
+        raises a ValueError. Returns (thetas (C, n_batch*batch_size, P), scales (C, n_batch, P),
+        accept_rates (C, n_batch))."""
         C = self.n_chains
         thetas = np.empty((C, n_batch * batch_size, self.P))
         scales = np.empty((C, n_batch, self.P))
@@ -671,8 +702,10 @@ class _BatchedMHMixin(object):
             lo, hi = b * batch_size, (b + 1) * batch_size
             thetas[:, lo:hi], n_reject = self.get_samples(batch_size, th0)
             if isinstance(n_reject, tuple):
-                if reject_count_index is None:
-                    raise ValueError('several rejection counts: pass reject_count_index')
+                if not reject_count_index:
+                    raise ValueError('several rejection counts and a falsy reject_count_index '
+                                     '(the reference ignores index 0, samplers.py:143): pass -1 '
+                                     'or another nonzero index')
                 n_reject = n_reject[reject_count_index]
             rates[:, b] = 1. - (n_reject * 1. / batch_size)
             th0 = thetas[:, hi - 1].copy()

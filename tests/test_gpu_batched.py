@@ -219,11 +219,17 @@ def test_batched_mi_mh_consistent_and_batch_invariant(gpu_available):
     th1, (nru1, nrt1) = one.get_samples(6, th0[1:2])
     np.testing.assert_array_equal(th1[0], th[1])
     assert nru1[0] == nru[1] and nrt1[0] == nrt[1]
-    with pytest.raises(ValueError):
-        smp.adaptive_run(th[:, -1], 3, 1, 0.15, 0.30, lambda b, n: 1.5)
-    ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5,
-                                      reject_count_index=1)
+    with pytest.raises(ValueError):  # a falsy index (the reference ignores 0)
+        smp.adaptive_run(th[:, -1], 3, 1, 0.15, 0.30, lambda b, n: 1.5, reject_count_index=0)
+    # the reference's default -1 adapts on the last count, the theta step (samplers.py:70, 143)
+    ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5)
     assert ath.shape == (4, 8, smp.P) and sc.shape == (4, 2, smp.P)
+    twin = S(X, y, 4, 16, prior, prop_scales=0.1, seed=61)
+    twin.get_samples(6, th0)
+    ath1, sc1, rates1 = twin.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5,
+                                          reject_count_index=1)
+    np.testing.assert_array_equal(rates1, rates)
+    np.testing.assert_array_equal(ath1, ath)
 
 
 def test_run_async_finish_mode_ends_on_boundaries(gpu_available, tmp_path):
@@ -244,6 +250,18 @@ def test_run_async_finish_mode_ends_on_boundaries(gpu_available, tmp_path):
         assert b.restore({k: z[k] for k in z.files}) == 0.
     tb, db = b.run_async(2)
     np.testing.assert_array_equal(np.array(ta), np.array(tb))
+    # u carried by the checkpoint itself (store_u): the replay history restarts there, the
+    # rejection counters travel, and the continuation is the same bit for bit
+    ck = a.checkpoint(store_u=True)
+    assert 'u' in ck and ck['ulog_n'].sum() == 0 and 'n_reject_u' in ck
+    np.savez(tmp_path / 'cku.npz', **ck)
+    ta2, _ = a.run_async(2)
+    _, _, _, c = _sampler(seed=71, chains=4)
+    with np.load(tmp_path / 'cku.npz') as z:
+        assert c.restore({k: z[k] for k in z.files}) == 0.
+    tc2, _ = c.run_async(2)
+    np.testing.assert_array_equal(np.array(ta2), np.array(tc2))
+    assert 'u' in c.checkpoint()  # later checkpoints keep carrying u
 
 
 def test_batched_mi_seqslice_consistent_and_batch_invariant(gpu_available):

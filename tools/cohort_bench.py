@@ -26,8 +26,11 @@ def run(K, a, X, y):
     smps = [BatchedAPMEllSSPlusRandDirSliceSampler(
         X, y, C, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
         seed=a.seed, first_chain=q * C) for q in range(K)]
-    for s in smps:
-        s.initialise()
+    th = None
+    if a.stationary:  # the long-chain record's chain states (bench.stationary_states)
+        th = np.load(a.stationary)[np.arange(a.chains) % 64]
+    for q, s in enumerate(smps):
+        s.initialise(None if th is None else th[q * C:(q + 1) * C])
 
     def par(fn):
         out = [None] * K
@@ -60,6 +63,8 @@ def main():
     ap.add_argument('--d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
+    ap.add_argument('--stationary', default=None,
+                    help='start from these chain states (profiles/r04_stationary_thetas.npy)')
     a = ap.parse_args()
     from gpdemo.utils import synthetic_gp_data
     X, y = synthetic_gp_data(a.n, a.d, a.seed)
