@@ -1,74 +1,91 @@
-// Microbenchmark of the fp32 trailing-update kernels (64x64 and 128x128 per workgroup) on random
-// data, Newton-matrix shape at N=4096 (development tool). Ablations of the 128x128 kernel:
-// -DT128_ABL=1 operands always slice 0, =2 no MFMA, =3 no operand loads.
-// hipcc --offload-arch=gfx950 -O3 -x hip tools/upd32_bench.cpp -o tools/upd32.bin
+// Microbenchmark of the Newton factorisation's rank-512 trailing update (k_chol_update32_t128,
+// fp16x3 operands) at the stationary theta-call shape: 64 chains, N = 4096, the outer panel K's
+// update of every tile column right of it (the appended right-hand-side row block included, as
+// in chol_range32). Development tool: prints ms per launch, fp32-equivalent TFLOP/s (lower
+// triangle, the bench's roofline accounting) and an output checksum (variants must match it).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/upd32_bench.cpp -o tools/upd32.bin
+//   tools/upd32.bin [chains=64] [K=0] [reps=10]
 #include "../auxiliary-pm-mcmc_amd/csrc/chol32.hip"
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
+#pragma clang diagnostic ignored "-Wunused-result"
 
-__global__ void fill(float* p, size_t n, unsigned seed) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        unsigned x = (unsigned)i * 2654435761u ^ seed;
-        x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
-        p[i] = ((float)(x & 0xffffff) / 16777216.0f - 0.5f) * 0.01f;
-    }
-}
-
-static double flops_of(int i0, int R, int j0, int jend, int kc) {
-    double f = 0;
+static double upd_flops(int i0, int R, int j0, int jend, int kc) {
+    double f = 0.0;
     for (int i = i0; i < R; ++i)
         for (int j = j0; j <= std::min(i, jend - 1); ++j)
-            f += (i == j) ? 64.0 * 65 * 64 * kc : 2.0 * 64 * 64 * 64 * kc;
+            f += (i == j) ? 64.0 * 65.0 * 64.0 * kc : 2.0 * 64.0 * 64.0 * 64.0 * kc;
     return f;
 }
 
 int main(int argc, char** argv) {
-    const int nb = 64, chains = argc > 1 ? atoi(argv[1]) : 64;
-    const int R = nb + 1, Cb = nb;
-    const int64_t ld = 64 * nb, rows = 64 * (nb + 1);
-    const int64_t cs = rows * ld;
+    const int chains = argc > 1 ? atoi(argv[1]) : 64, K = argc > 2 ? atoi(argv[2]) : 0;
+    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const int np = 4096, nb = np / 64, outer = 8;
+    const int64_t ld = np, cs = (int64_t)(np + 64) * np;
     float* A;
-    if (hipMalloc(&A, sizeof(float) * cs * chains) != hipSuccess) { printf("oom\n"); return 1; }
-    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, A, (size_t)cs * chains, 7u);
-    int *act, *st;
-    hipMalloc(&act, 4 * chains); hipMalloc(&st, 4 * chains);
+    hipMalloc(&A, sizeof(float) * cs * chains);
+    float* A0;
+    hipMalloc(&A0, sizeof(float) * cs * chains);
+    std::vector<float> h((size_t)cs);
+    srand(7);
+    for (int b = 0; b < chains; ++b) {
+        for (int64_t e = 0; e < cs; ++e) {
+            const int64_t r = e / ld;
+            h[e] = (r >= np && r != np) ? 0.f : (float)((rand() / (double)RAND_MAX - 0.5) * 2.0);
+        }
+        hipMemcpy(A0 + b * cs, h.data(), sizeof(float) * cs, hipMemcpyHostToDevice);
+    }
+    int *act, *st, *h3;
+    hipMalloc(&act, 4 * chains);
+    hipMalloc(&st, 4 * chains);
+    hipMalloc(&h3, 4 * chains);
     std::vector<int> one(chains, 1), zero(chains, 0);
     hipMemcpy(act, one.data(), 4 * chains, hipMemcpyHostToDevice);
     hipMemcpy(st, zero.data(), 4 * chains, hipMemcpyHostToDevice);
-    MatF M{A, ld, cs};
-    Live lv{act, st};
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0); hipEventCreate(&e1);
-    struct Cfg { int k0, kc, i0; const char* name; };
-    Cfg cfgs[] = {{0, 4, 4, "outer K=0 rank256"}, {32, 4, 36, "outer K=32 rank256"},
-                  {0, 8, 8, "outer K=0 rank512"}};
-    for (const Cfg& c : cfgs) {
-        for (int ker = 0; ker < 2; ++ker) {
-            std::vector<unsigned> t = ker ? build_update_supertiles(c.i0, R, c.i0, Cb, 0, 0)
-                                          : build_update_tiles(c.i0, R, c.i0, Cb);
-            unsigned* dt;
-            hipMalloc(&dt, 4 * t.size());
-            hipMemcpy(dt, t.data(), 4 * t.size(), hipMemcpyHostToDevice);
-            auto run = [&]() {
-                if (ker) launch_chol_update32_t128(M, c.k0, c.kc, dt, (int)t.size(), lv, chains, 0);
-                else launch_chol_update32(M, c.k0, c.kc, dt, (int)t.size(), lv, chains, 0);
-            };
-            for (int w = 0; w < 2; ++w) run();
-            hipEventRecord(e0);
-            const int reps = 5;
-            for (int w = 0; w < reps; ++w) run();
-            hipEventRecord(e1);
-            hipEventSynchronize(e1);
-            float ms;
-            hipEventElapsedTime(&ms, e0, e1);
-            const double fl = flops_of(c.i0, R, c.i0, Cb, c.kc) * chains * reps;
-            printf("ABL=%d %-8s %-20s tiles %6zu x %d: %8.3f ms/launch %7.2f TFLOP/s\n", T128_ABL,
-                   ker ? "128x128" : "64x64", c.name, t.size(), chains, ms / reps,
-                   fl / (ms * 1e-3) / 1e12);
-            hipFree(dt);
+    hipMemcpy(h3, one.data(), 4 * chains, hipMemcpyHostToDevice);
+    const int k0 = K * outer, kc = outer, Kend = k0 + kc, R = nb + 1, rhs = nb;
+    std::vector<unsigned> sl = build_update_supertiles(Kend, R, Kend, nb, 0, 0, rhs);
+    unsigned* dsl;
+    hipMalloc(&dsl, sizeof(unsigned) * sl.size());
+    hipMemcpy(dsl, sl.data(), sizeof(unsigned) * sl.size(), hipMemcpyHostToDevice);
+    const MatF M{A, ld, cs};
+    const Live lv{act, st};
+    const FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
+    auto launch = [&]() {
+        launch_chol_update32_t128(M, k0, kc, dsl, (int)sl.size(), lv, chains, nullptr, fd, nb, h3,
+                                  rhs);
+    };
+    // checksum of one launch from the pristine matrix
+    hipMemcpy(A, A0, sizeof(float) * cs * chains, hipMemcpyDeviceToDevice);
+    launch();
+    hipDeviceSynchronize();
+    std::vector<float> out((size_t)cs);
+    double sum = 0.0;
+    unsigned long long hsh = 1469598103934665603ull;
+    for (int b = 0; b < chains; b += std::max(1, chains / 4)) {
+        hipMemcpy(out.data(), A + b * cs, sizeof(float) * cs, hipMemcpyDeviceToHost);
+        for (int64_t e = 0; e < cs; ++e) {
+            sum += std::fabs((double)out[e]);
+            unsigned u;
+            std::memcpy(&u, &out[e], 4);
+            hsh = (hsh ^ u) * 1099511628211ull;
         }
     }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int w = 0; w < 2; ++w) launch();
+    hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; ++r) launch();
+    hipEventRecord(e1, nullptr);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double fl = upd_flops(Kend, R - 1, Kend, nb, kc) * chains;  // (rhs row: not credited)
+    printf("K=%d chains=%d supertiles=%zu: %.4f ms/launch  %.1f TFLOP/s fp32-eq  sum %.9e hash "
+           "%016llx\n", K, chains, sl.size(), ms / reps, fl / (ms / reps * 1e-3) / 1e12, sum, hsh);
     return 0;
 }
