@@ -90,23 +90,13 @@ struct SpinCtl {
     unsigned long long* timeouts;  // bounded-spin exits (APM_PROF_DF / _TRSV_TIMEOUTS)
     int limit;                     // polls before a wait gives up
 };
-// fp16 operand planes of the Newton factorisation's outer panels for the trailing update's GEMM
-// (chol32.hip store_planes): per chain, per row PLANE_W halves [lo | hi | hi | lo] of the panel's
-// 512 columns; written by the dataflow panel launch for row tiles < rows (the GEMM's rows)
-#define PLANE_W 2048
-struct Planes {
-    _Float16* base;
-    int64_t cstride;
-    int rows;
-};
 // tile columns [K, K+ncols) of an outer panel (diagonal tile (K, K) already factored) in one
 // dataflow launch (chol32.hip: per-(chain, row) progress words prog[b * pstride + row], monotonic
 // base per factorisation and panel); returns the launch's workgroup count (its tickets), 0 when
 // nothing was launched, -1 for a panel wider than the progress word allows
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, SpinCtl sc, Planes pl,
-                            hipStream_t s);
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s);
 // rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is final (fd.Dinv: its
 // inverses), each row a left-looking walk over the panel's columns with no waits; zrow > 0: row
 // tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)
@@ -126,9 +116,7 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
-                               int hlim = 0, const int* h3ok = nullptr, int rhs = -1,
-                               const int* sel = nullptr, int selv = -1);
-// (sel != nullptr: only the chains b with (sel[b] != 0) == (selv != 0))
+                               int hlim = 0, const int* h3ok = nullptr, int rhs = -1);
 // solo >= 0: row tile solo gets super-tile rows of its own (never paired with another row tile)
 std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
                                               int solo = -1);

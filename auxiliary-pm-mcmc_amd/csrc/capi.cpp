@@ -5,7 +5,6 @@
 //   check } -> augmented chol [[B,.],[K W^1/2, K],[0, f_post^T]] -> slot -> L.U + probit -> LME
 // The only host syncs are one per Newton iteration (convergence flags) and one at the end.
 #include <hip/hip_runtime.h>
-#include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -116,19 +115,6 @@ struct apm_ctx {
     // start of every theta-call, ticket_base = the tickets the call's launches have drawn so far
     unsigned long long ticket_base = 0;
     int spin_df = 1 << 22, spin_trsv = 1 << 20;  // poll bounds (APM_SPIN_LIMIT: tests only)
-    // Newton trailing updates as hipBLASLt fp16 GEMMs on the operand planes the dataflow panel
-    // writes (APM_GEMM=1; launch_update_gemm): planes = B x np x PLANE_W halves
-    bool gemm = false;
-    _Float16* planes = nullptr;
-    int64_t plane_cs = 0;
-    void* blt_ws = nullptr;
-    size_t blt_wsz = 0;
-    struct GemmPlan {
-        hipblasLtMatmulDesc_t d;
-        hipblasLtMatrixLayout_t a, b, c;
-        hipblasLtMatmulAlgo_t algo;
-    };
-    std::map<std::tuple<int, int, int>, GemmPlan> gemm_plans;  // (rows, cols, batch)
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
     // previous convergence read; update_flops x live_n instead of x count)
     int live_n = 0;
@@ -436,126 +422,6 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     check_launch();
 }
 
-// ---- the Newton trailing update as hipBLASLt GEMMs (APM_GEMM=1) ---------------------------------
-// One hipBLASLt handle per device, shared by the contexts (its creation loads the kernel library)
-std::mutex g_blt_mu;
-std::map<int, hipblasLtHandle_t> g_blt;
-hipblasLtHandle_t blt_handle(apm_ctx* c) {
-    std::lock_guard<std::mutex> lk(g_blt_mu);
-    auto it = g_blt.find(c->device);
-    if (it != g_blt.end()) return it->second;
-    hipblasLtHandle_t h = nullptr;
-    if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) throw HipError{"hipblasLtCreate failed"};
-    g_blt[c->device] = h;
-    return h;
-}
-#define BLTC(x)                                                                          \
-    do {                                                                                 \
-        if ((x) != HIPBLAS_STATUS_SUCCESS) throw HipError{std::string("hipBLASLt: ") + #x}; \
-    } while (0)
-
-// the trailing update of an outer panel goes to the GEMMs when the context enables them, some
-// chain of the call takes fp16x3 operands and a column block is left to update
-// (the GEMM's contraction depth is the planes' 3 x 512: full-width outer panels only)
-bool use_gemm(apm_ctx* c, int K, int Kend, int Cb) {
-    return c->gemm && c->h3_now && Kend < Cb && Kend - K == 8;
-}
-
-// C (rows r0 .. np of block column [j0, j0 + cols), fp32 row-major) -= Lw Rw^T over the batch:
-// in hipBLASLt's column-major view D (cols x rows) = A^T B with A = the block column's rows'
-// right windows (K' x cols, ld PLANE_W), B = the rows' left windows (K' x rows)
-apm_ctx::GemmPlan& gemm_plan(apm_ctx* c, int rows, int cols, int batch) {
-    auto key = std::make_tuple(rows, cols, batch);
-    auto it = c->gemm_plans.find(key);
-    if (it != c->gemm_plans.end()) return it->second;
-    hipblasLtHandle_t h = blt_handle(c);
-    apm_ctx::GemmPlan g{};
-    const int KP = 1536;
-    BLTC(hipblasLtMatmulDescCreate(&g.d, HIPBLAS_COMPUTE_32F, HIP_R_32F));
-    hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
-    BLTC(hipblasLtMatmulDescSetAttribute(g.d, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
-    BLTC(hipblasLtMatmulDescSetAttribute(g.d, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
-    BLTC(hipblasLtMatrixLayoutCreate(&g.a, HIP_R_16F, KP, cols, PLANE_W));
-    BLTC(hipblasLtMatrixLayoutCreate(&g.b, HIP_R_16F, KP, rows, PLANE_W));
-    BLTC(hipblasLtMatrixLayoutCreate(&g.c, HIP_R_32F, cols, rows, c->np));
-    int32_t bc = batch;
-    int64_t sp = c->plane_cs, sc = 2 * c->A.cstride;  // (b32_of: fp32 chain stride)
-    for (auto L : {g.a, g.b, g.c})
-        BLTC(hipblasLtMatrixLayoutSetAttribute(L, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc,
-                                               sizeof(bc)));
-    BLTC(hipblasLtMatrixLayoutSetAttribute(g.a, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sp,
-                                           sizeof(sp)));
-    BLTC(hipblasLtMatrixLayoutSetAttribute(g.b, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sp,
-                                           sizeof(sp)));
-    BLTC(hipblasLtMatrixLayoutSetAttribute(g.c, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sc,
-                                           sizeof(sc)));
-    hipblasLtMatmulPreference_t pref;
-    BLTC(hipblasLtMatmulPreferenceCreate(&pref));
-    BLTC(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
-                                               &c->blt_wsz, sizeof(c->blt_wsz)));
-    hipblasLtMatmulHeuristicResult_t res[4];
-    int nres = 0;
-    BLTC(hipblasLtMatmulAlgoGetHeuristic(h, g.d, g.a, g.b, g.c, g.c, pref, 4, res, &nres));
-    hipblasLtMatmulPreferenceDestroy(pref);
-    if (nres <= 0) throw HipError{"hipBLASLt: no algorithm for the Newton update GEMM"};
-    g.algo = res[0].algo;
-    return c->gemm_plans.emplace(key, g).first->second;
-}
-
-int* pin_h3(apm_ctx* c);
-
-// The trailing update of the Newton matrix after the outer panel [K, Kend) (chol_range32): the
-// lower block triangle of rows / columns [Kend, nb) as one strided-batched fp16 GEMM per 512-wide
-// block column on the planes the dataflow launch wrote (lo.hi + hi.hi + hi.lo accumulated in
-// fp32: the fp16x3 product of k_chol_update32_t128, in hipBLASLt's summation order); the appended
-// right-hand-side row and any chain without fp16x3 operands (its planes are zero, so the GEMM
-// leaves it unchanged) through k_chol_update32_t128 with fp32 operands; then the next diagonal
-// tile (the fused step of the kernel path) by its own launch. The GEMM computes every chain of the
-// call: converged or failed chains only receive values nothing reads again.
-void gemm_update32(apm_ctx* c, MatF M, int K, int Kend, int R, int Cb, int count, bool have_diag,
-                   int fail_code) {
-    const int kc = Kend - K, nb = c->nb;
-    const double fl = c->prof ? update_flops(Kend, R, Kend, Cb, kc, Gap{0, 0}) * c->live_n : 0.0;
-    {
-        ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
-        ProfScope ps_outer(c, APM_PROF_CHOL_UPDATE32_OUTER, fl);
-        hipblasLtHandle_t h = blt_handle(c);
-        const float alpha = -1.f, beta = 1.f;
-        for (int j0 = Kend; j0 < Cb; j0 += c->outer32) {
-            const int cols = 64 * std::min(c->outer32, Cb - j0);
-            const int r0 = 64 * j0, rows = 64 * nb - r0;  // (the rhs row block nb excluded)
-            apm_ctx::GemmPlan& g = gemm_plan(c, rows, cols, count);
-            const _Float16* pr = c->planes + (int64_t)r0 * PLANE_W;
-            float* C = M.base + (int64_t)r0 * M.ld + r0;
-            BLTC(hipblasLtMatmul(h, g.d, &alpha, pr + 512, g.a, pr, g.b, &beta, C, g.c, C, g.c,
-                                 &g.algo, c->blt_ws, c->blt_wsz, c->stream));
-        }
-    }
-    // the rhs row (and, for a chain without fp16x3 operands, every tile: fp32 operands)
-    bool all_h3 = true;
-    for (int b = 0; b < count; ++b) all_h3 &= pin_h3(c)[b] != 0;
-    const int rhs = R > nb ? nb : -1;
-    if (!all_h3) {
-        const auto sl = super_list(c, Kend, R, Kend, Cb, Gap{0, 0}, rhs);
-        launch_chol_update32_t128(M, K, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, 0, nullptr,
-                                  rhs, c->h3ok, 0);  // chains with h3ok == 0 only
-        check_launch();
-    }
-    if (rhs >= 0) {
-        const auto sl = super_list(c, nb, R, Kend, Cb, Gap{0, 0}, rhs);
-        launch_chol_update32_t128(M, K, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, 0, nullptr,
-                                  rhs, all_h3 ? nullptr : c->h3ok, 1);  // the others' rhs row
-        check_launch();
-    }
-    if (have_diag) {
-        launch_chol_diag32(M, Kend, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, live_of(c),
-                           fail_code, count, c->stream);
-        check_launch();
-    }
-}
-
 // chol_range's twin for the fp32 Newton matrix (same steps, same fused diag)
 void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_code, int count) {
     const Live lv = live_of(c);
@@ -575,18 +441,13 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                 M, K, Kend - K, R, FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
                 count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
                 (fact << 16) | ((unsigned long long)(K / c->outer32) << 4), spin_ctl(c, false),
-                use_gemm(c, K, Kend, Cb) ? Planes{c->planes, c->plane_cs, c->nb}
-                                      : Planes{nullptr, 0, 0},
                 c->stream);
             if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
             c->ticket_base += (unsigned long long)tickets;
             have_diag = Kend < k1;
-            if (use_gemm(c, K, Kend, Cb))
-                gemm_update32(c, M, K, Kend, R, Cb, count, have_diag, fail_code);
-            else
-                tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count,
-                                 have_diag ? Kend : -1, fail_code);
+            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
+                             fail_code);
             continue;
         }
         // APM_DF32=0: the launch sequence the dataflow kernel replaces (left-looking inside the
@@ -1256,7 +1117,6 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
-    if (const char* e = getenv("APM_GEMM")) c->gemm = atoi(e) != 0;
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1362,15 +1222,6 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->slot_wide.assign((size_t)n_slots, 0);
     c->Up = UPool{dalloc<double>(c, n_ubufs * np * c->sp), np * c->sp, c->sp,
                   dalloc<float>(c, n_ubufs * np * c->sp)};
-    if (c->gemm && c->df32 && c->mixed) {  // operand planes + workspace of the update GEMMs
-        c->plane_cs = np * PLANE_W;
-        c->planes = dalloc<_Float16>(c, (size_t)B * c->plane_cs);
-        HIPC(hipMemset(c->planes, 0, sizeof(_Float16) * B * c->plane_cs));
-        c->blt_wsz = 32ull << 20;
-        c->blt_ws = dalloc<char>(c, c->blt_wsz);
-    } else {
-        c->gemm = false;
-    }
     HIPC(hipMemset(c->Up.base, 0, sizeof(double) * n_ubufs * np * c->sp));
     HIPC(hipMemset(c->Up.base32, 0, sizeof(float) * n_ubufs * np * c->sp));
 }
@@ -1391,12 +1242,6 @@ void free_ctx(apm_ctx* c) {
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_gram) (void)hipEventDestroy(c->ev_gram);
     if (c->ev_cholk) (void)hipEventDestroy(c->ev_cholk);
-    for (auto& kv : c->gemm_plans) {
-        hipblasLtMatrixLayoutDestroy(kv.second.a);
-        hipblasLtMatrixLayoutDestroy(kv.second.b);
-        hipblasLtMatrixLayoutDestroy(kv.second.c);
-        hipblasLtMatmulDescDestroy(kv.second.d);
-    }
     for (hipEvent_t e : c->ev_feed)
         if (e) (void)hipEventDestroy(e);
     delete c;

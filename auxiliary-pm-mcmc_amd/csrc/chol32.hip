@@ -371,40 +371,6 @@ __device__ __forceinline__ void tile32_store_sc1(const f4_t (&acc)[2][2], float*
 #ifndef DF_BULK_WPE
 #define DF_BULK_WPE 3  // ... and of its bulk-row twin (no diagonal factorisation, no waits)
 #endif
-// fp16 operand planes of a row's final panel tiles for the trailing update's GEMM
-// (gemm_update32, capi.cpp): the chain's plane buffer holds per row [lo | hi | hi | lo] of the
-// outer panel's 512 columns (hi = fp16(x), lo = fp16(x - hi), split_h3's split), so that the
-// windows [0, 1536) and [512, 2048) of two rows contract to lo.hi + hi.hi + hi.lo - the fp16x3
-// product of k_chol_update32_t128 - in one K' = 1536 fp16 GEMM. Run by a bulk row's workgroup
-// after its walk (its tiles are final and were stored by this workgroup; read back as the walk
-// reads its own earlier tiles), with few live registers: thread t converts 8-column runs of the
-// 64 x (64 ncols) block. zero: a chain whose update takes fp32 operands (h3ok == 0) gets zero
-// planes (its GEMM term vanishes).
-__device__ __forceinline__ void store_planes(const float* Ai, int64_t ld, int ncols, _Float16* dst,
-                                             bool zero) {
-    __syncthreads();  // every wave's tile stores are done
-    const int runs = 8 * ncols;  // 8-column runs per row
-#pragma unroll 1
-    for (int q = threadIdx.x; q < 64 * runs; q += 256) {
-        const int row = q / runs, c = 8 * (q % runs);
-        const f4_t v0 = *reinterpret_cast<const f4_t*>(Ai + (int64_t)row * ld + c);
-        const f4_t v1 = *reinterpret_cast<const f4_t*>(Ai + (int64_t)row * ld + c + 4);
-        h8_t hi, lo;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float v = zero ? 0.f : (e < 4 ? v0[e] : v1[e - 4]);
-            const _Float16 xh = (_Float16)v;
-            hi[e] = xh;
-            lo[e] = (_Float16)(v - (float)xh);
-        }
-        _Float16* d = dst + (int64_t)row * PLANE_W + c;
-        *reinterpret_cast<h8_t*>(d) = lo;
-        *reinterpret_cast<h8_t*>(d + 512) = hi;
-        *reinterpret_cast<h8_t*>(d + 1024) = hi;
-        *reinterpret_cast<h8_t*>(d + 1536) = lo;
-    }
-}
-
 // BULK = false: rows [K, R) as described above. BULK = true: rows [row0, R) below an outer panel
 // whose diagonal block is already factored (every diagonal tile and its inverse final): the same
 // row walk without the waits and without the diagonal factorisation code (whose registers hold
@@ -418,7 +384,7 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          unsigned long long* prog,
                                                          int64_t pstride,
                                                          unsigned long long base, SpinCtl sc,
-                                                         Planes pl, int row0 = 0, int zrow = 0) {
+                                                         int row0 = 0, int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -656,23 +622,18 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
             __syncthreads();  // the staging area is reused by the next column's update
         }
     }
-    // (only rows below the diagonal block get here: a row of the trailing update's GEMM)
-    if (!BULK && pl.base && i < pl.rows)
-        store_planes(Ai + K * 64, A.ld, ncols,
-                     pl.base + b * pl.cstride + (int64_t)(i * 64) * PLANE_W, !h3);
 }
 
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, SpinCtl sc, Planes pl,
-                            hipStream_t s) {
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s) {
     // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
     // caller raises) instead of being left unfactored
     if (ncols > 14) return -1;
     if (ncols < 1 || R - K <= 1) return 0;  // (one column: its panel TRSM)
     const long grid = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
-                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc, pl);
+                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc);
     return grid;
 }
 
@@ -682,8 +643,7 @@ void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zro
     if (ncols < 1 || R <= row0) return;
     hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
-                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0},
-                       Planes{nullptr, 0, 0}, row0, zrow);
+                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0}, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -779,9 +739,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
                                                                int ntiles, int nchains, Live live,
                                                                FusedDiag<float> fd, int hlim,
                                                                const int* __restrict__ h3ok,
-                                                               int rhs,
-                                                               const int* __restrict__ sel,
-                                                               int selv) {
+                                                               int rhs) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     __shared__ union {
@@ -802,7 +760,6 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
         t = (int)(w % nt) + (fd.enabled ? 1 : 0);
     }
     if (!live32(live, b)) return;
-    if (sel && (sel[b] != 0) != (selv != 0)) return;  // chain selection (gemm_update32)
     const unsigned e = tiles[t];
     const int ti = (int)(e >> 18), tj = (int)((e >> 4) & 0x3fff);
     const bool rv0 = e & 1u, rv1 = e & 2u, cv0 = e & 4u, cv1 = e & 8u;
@@ -1023,15 +980,15 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
-                               int hlim, const int* h3ok, int rhs, const int* sel, int selv) {
+                               int hlim, const int* h3ok, int rhs) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
     if (hlim > 0)
         hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs, sel, selv);
+                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs);
     else
         hipLaunchKernelGGL(k_chol_update32_t128<false>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr, rhs, sel, selv);
+                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr, rhs);
 }
 
 // Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),

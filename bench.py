@@ -17,6 +17,7 @@ timed region; `cpu_baseline` times the CPU restatement of the reference (oracle/
 """
 import argparse
 import json
+import types
 import os
 import sys
 import time
@@ -46,7 +47,7 @@ def parse():
     ap.add_argument('--d', '--n-features', dest='d', type=int, default=32)
     ap.add_argument('--n-imp', type=int, default=256)
     ap.add_argument('--seed', type=int, default=20151009)
-    ap.add_argument('--schedule', choices=('async', 'lockstep'), default='async',
+    ap.add_argument('--schedule', choices=('async',), default='async',
                     help='chain scheduling of the batched sampler (auxpm/batched.py)')
     ap.add_argument('--cpu-baseline', type=int, default=1)
     ap.add_argument('--cpu-budget', type=float, default=30.0,
@@ -56,6 +57,10 @@ def parse():
                          "reference's own full-size fixture); exit 3 on a failure")
     ap.add_argument('--ess-min', type=int, default=100,
                     help='post-burn-in transitions per chain for the ESS (untimed extension)')
+    ap.add_argument('--cohorts', type=int, default=1,
+                    help='split each rank\'s chains into this many device contexts driven by '
+                         'their own host threads (Cohorts): one cohort\'s latency-bound Newton '
+                         'phases overlap another\'s MFMA-bound posterior factor')
     ap.add_argument('--ess-burn', type=int, default=50,
                     help='transitions discarded from the start of each chain for the ESS '
                          '(at least --warmup)')
@@ -640,6 +645,93 @@ def ess_long_record(value, a):
                     '(ess_per_sec_record)'}
 
 
+class Cohorts(object):
+    """The rank's chains as K cohorts of n_chains / K chains, each its own sampler and device
+    context (own HIP streams) advanced by its own host thread (ctypes calls release the GIL), so
+    that the GPU overlaps one cohort's latency-bound Newton phases (TRSVs, dataflow diagonal
+    chains, host round trips) with another's MFMA-bound work. Cohort q holds chains
+    [q C, (q + 1) C) with the streams of those chains of one n_chains sampler (first_chain), so
+    every chain's trajectory is the one it has in a single batch (batch invariance,
+    tests/test_gpu_batched.py). Presents the sampler interface bench.py uses."""
+
+    def __init__(self, make, n_chains, k):
+        import threading
+        self.threading = threading
+        self.k = k
+        self.C = n_chains // k
+        self.parts = [make(self.C, q * self.C) for q in range(k)]
+        self.n_chains = n_chains
+        self.P = self.parts[0].P
+
+    def _par(self, fn):
+        out = [None] * self.k
+        err = []
+
+        def run(q):
+            try:
+                out[q] = fn(q, self.parts[q])
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+        ths = [self.threading.Thread(target=run, args=(q,)) for q in range(self.k)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if err:
+            raise err[0]
+        return out
+
+    def initialise(self, theta_init=None):
+        self._par(lambda q, s: s.initialise(
+            None if theta_init is None else theta_init[q * self.C:(q + 1) * self.C]))
+
+    def run_async(self, n_steps, keep_going=False):
+        n = np.broadcast_to(np.asarray(n_steps, dtype=np.int64), (self.n_chains,))
+        res = self._par(lambda q, s: s.run_async(n[q * self.C:(q + 1) * self.C], keep_going))
+        return [t for r in res for t in r[0]], np.concatenate([r[1] for r in res])
+
+    @property
+    def failed(self):
+        return np.concatenate([s.failed for s in self.parts])
+
+    @property
+    def ctxs(self):
+        return [s.ctx for s in self.parts]
+
+    def __getattr__(self, name):  # counters and records summed / concatenated over cohorts
+        parts = self.__dict__.get('parts')
+        if parts is None:
+            raise AttributeError(name)
+        if name in ('n_theta_calls', 'n_u_calls'):
+            return sum(getattr(s, name) for s in parts)
+        if name == 'call_ops':
+            return [o for s in parts for o in s.call_ops]
+        if name == 'wall':
+            return {k: sum(s.wall[k] for s in parts) for k in parts[0].wall}
+        raise AttributeError(name)
+
+    def reset_records(self):
+        for s in self.parts:
+            s.call_ops = []
+            for k in s.wall:
+                s.wall[k] = 0.
+            for h in s.ctx.batch_hist.values():
+                h.clear()
+
+    def batch_hist(self):
+        out = {}
+        for s in self.parts:
+            for kind, h in s.ctx.batch_hist.items():
+                d = out.setdefault(kind, {})
+                for size, n in h.items():
+                    d[size] = d.get(size, 0) + n
+        return {k: dict(sorted(v.items())) for k, v in out.items()}
+
+    def close(self):
+        for s in self.parts:
+            s.ctx.close()
+
+
 def run_chains(a, dist, dev, X, y, theta_init, measure):
     """One batched-chain run of the benchmark workload on this rank's device: `--warmup`
     untimed transitions per chain, then the timed region (every chain completes >= `--steps`
@@ -650,55 +742,42 @@ def run_chains(a, dist, dev, X, y, theta_init, measure):
     from auxpm.batched import BatchedAPMEllSSPlusRandDirSliceSampler
     from gpdemo import _native
     prior = dict(a_tau=1., b_tau=1. / a.d ** 0.5, a_sigma=1.1, b_sigma=0.1)
-    smp = BatchedAPMEllSSPlusRandDirSliceSampler(
-        X, y, a.chains, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
-        seed=chain_seed(a.seed, dist.rank), device=dev)
+    if a.chains % a.cohorts:
+        raise SystemExit('bench.py: --chains must be a multiple of --cohorts')
+    smp = Cohorts(lambda C, first: BatchedAPMEllSSPlusRandDirSliceSampler(
+        X, y, C, a.n_imp, prior, kernel='ard', epsilon=1e-8, w=1., max_steps_out=0,
+        seed=chain_seed(a.seed, dist.rank), device=dev, first_chain=first), a.chains, a.cohorts)
     smp.initialise(theta_init)
     series = [[] for _ in range(a.chains)]  # every transition of each chain (ESS)
-    if a.schedule == 'async':
-        if a.warmup:
-            # every chain W transitions, ending on a transition boundary
-            wtr, _ = smp.run_async(a.warmup)
-            for c in range(a.chains):
-                series[c].extend(wtr[c])
-    else:
-        for _ in range(a.warmup):
-            th = smp.step()
-            for c in range(a.chains):
-                series[c].append(th[c].copy())
-    ctx = smp.ctx
-    for k in range(_native.PROF_NKINDS):
-        ctx.prof_read(k, reset=True)
-    if measure:
-        # roofline level: one HIP-event pair per Gram, L.U and rank-512 update launch (the
-        # in-panel update launches are not bracketed: their events cost ~2 % of the theta-call)
-        ctx.prof_enable(1)
-    device_sync()  # first torch touch outside the timed region
-    mark = (lambda: ctx.prof_marker(1)) if measure else None  # window bracket (prof_window.py)
-    th0, u0 = smp.n_theta_calls, smp.n_u_calls
-    smp.call_ops = []
-    for h in ctx.batch_hist.values():
-        h.clear()
-    for k in smp.wall:
-        smp.wall[k] = 0.
-    res = {}
-    if a.schedule == 'async':
-        def body():
-            res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
-        elapsed = timed_region(dist, body, 1, mark)
-        done = res['done']
+    if a.warmup:
+        # every chain W transitions, ending on a transition boundary
+        wtr, _ = smp.run_async(a.warmup)
         for c in range(a.chains):
-            series[c].extend(res['traces'][c])
-    else:
-        def one_step():
-            th = smp.step()
-            for c in range(a.chains):
-                series[c].append(th[c].copy())
-        elapsed = timed_region(dist, one_step, a.steps, mark)
-        done = np.where(smp.failed, 0, a.steps)
+            series[c].extend(wtr[c])
+    for ctx in smp.ctxs:
+        for k in range(_native.PROF_NKINDS):
+            ctx.prof_read(k, reset=True)
+        if measure:
+            # roofline level: one HIP-event pair per Gram, L.U and rank-512 update launch (the
+            # in-panel update launches are not bracketed: their events cost ~2 % of the
+            # theta-call)
+            ctx.prof_enable(1)
+    device_sync()  # first torch touch outside the timed region
+    mark = (lambda: smp.ctxs[0].prof_marker(1)) if measure else None  # (tools/prof_window.py)
+    th0, u0 = smp.n_theta_calls, smp.n_u_calls
+    smp.reset_records()
+    res = {}
+
+    def body():
+        res['traces'], res['done'] = smp.run_async(a.steps, keep_going=True)
+    elapsed = timed_region(dist, body, 1, mark)
+    done = res['done']
+    for c in range(a.chains):
+        series[c].extend(res['traces'][c])
     if measure:
-        ctx.prof_marker(2)
-        ctx.prof_enable(False)
+        smp.ctxs[0].prof_marker(2)
+        for ctx in smp.ctxs:
+            ctx.prof_enable(False)
     done = np.where(smp.failed, 0, done)
     local_tr = int(done.sum())
     transitions = dist.sum(local_tr)
@@ -707,8 +786,7 @@ def run_chains(a, dist, dev, X, y, theta_init, measure):
            'value': transitions / elapsed, 'series': series,
            'n_th': (smp.n_theta_calls - th0) / max(1, local_tr),
            'n_u': (smp.n_u_calls - u0) / max(1, local_tr),
-           'call_ops': call_ops, 'wall': dict(smp.wall),
-           'batch_hist': {k: dict(sorted(v.items())) for k, v in ctx.batch_hist.items()},
+           'call_ops': call_ops, 'wall': dict(smp.wall), 'batch_hist': smp.batch_hist(),
            'theta_call_ms_mean': 1e3 * smp.wall['theta_call'] / max(1, len(call_ops))}
     return smp, rec
 
@@ -731,7 +809,6 @@ def main():
     # a whole chain is made of); where no record fits the workload, from prior draws
     th_stat, stat_src = stationary_states(a, P)
     smp, run = run_chains(a, dist, dev, X, y, th_stat, measure=True)
-    ctx = smp.ctx
     elapsed, done, local_tr = run['elapsed'], run['done'], run['local_tr']
     transitions, value = run['transitions'], run['value']
     n_th, n_u, call_ops, wall = run['n_th'], run['n_u'], run['call_ops'], run['wall']
@@ -742,9 +819,11 @@ def main():
                     (_native.PROF_UGEMM, 'ugemm'),
                     (_native.PROF_CHOL_UPDATE32_OUTER, 'chol_update32'),
                     (_native.PROF_POST32_OUTER, 'post32')):
-        prof[name] = ctx.prof_read(k, reset=False)
-    ctx.prof_read(0, reset=True)
-    n_rerun, n_refine, n_df_timeouts, n_trsv_timeouts, n_post64 = device_counters(ctx)
+        prof[name] = tuple(np.sum([ctx.prof_read(k, reset=False) for ctx in smp.ctxs], axis=0))
+    for ctx in smp.ctxs:
+        ctx.prof_read(0, reset=True)
+    n_rerun, n_refine, n_df_timeouts, n_trsv_timeouts, n_post64 = np.sum(
+        [device_counters(ctx) for ctx in smp.ctxs], axis=0)
 
     def mfma_roofline(name, kernel, peak, shorts, kind):
         ms, cnt, flops = prof[name]
@@ -836,24 +915,21 @@ def main():
     need = np.array([0 if smp.failed[c] else max(0, burn + a.ess_min - len(series[c]))
                      for c in range(a.chains)], dtype=np.int64)
     t_ext = time.perf_counter()
-    if need.max() > 0 and a.schedule == 'async':
+    if need.max() > 0:
         etr, _ = smp.run_async(need)
         for c in range(a.chains):
             series[c].extend(etr[c])
-    elif need.max() > 0:
-        for _ in range(int(need.max())):
-            th = smp.step()
-            for c in range(a.chains):
-                series[c].append(th[c].copy())
     t_ext = time.perf_counter() - t_ext
-    ess = ess_block(dist, smp, series, done, burn, elapsed, P)
+    failed_mask = smp.failed
+    ess = ess_block(dist, types.SimpleNamespace(n_chains=a.chains, failed=failed_mask), series,
+                    done, burn, elapsed, P)
     ess['sample']['untimed_extension_s_rank0'] = t_ext
     ess["sample"]["timed_transitions_per_chain_min"] = int(-dist.max(
-        -(done[~smp.failed].min() if (~smp.failed).any() else 0)))
+        -(done[~failed_mask].min() if (~failed_mask).any() else 0)))
     ess['sample']['timed_transitions_per_chain_max'] = int(dist.max(done.max()))
-    failed = int(dist.sum(int(smp.failed.sum())))
-    local_failed = int(smp.failed.sum())
-    ctx.close()  # frees the chains' workspaces before the next context
+    failed = int(dist.sum(int(failed_mask.sum())))
+    local_failed = int(failed_mask.sum())
+    smp.close()  # frees the chains' workspaces before the next context
 
     # the same workload from prior draws (the reference notebooks' chain start,
     # E-SS+RD-SS.ipynb:198-201): its first transitions need ~4 Newton iterations per theta-call
@@ -870,7 +946,7 @@ def main():
                           float(np.mean([m for m, _ in run2['call_ops']]))
                           if run2['call_ops'] else None,
                       'failed_chains': int(dist.sum(int(smp2.failed.sum())))}
-        smp2.ctx.close()
+        smp2.close()
 
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     cpu, first = None, None
@@ -920,6 +996,7 @@ def main():
                    'chains_per_gpu': a.chains, 'global_batch': a.chains * dist.world,
                    'parallelism': 'dp{0} (independent chains per GPU, no collective)'
                    .format(dist.world),
+                   'cohorts_per_gpu': a.cohorts,
                    'chain_start': ('stationary: the long-chain record\'s chain states ({0}), '
                                    'fresh u, then --warmup transitions'.format(stat_src)
                                    if stationary else
