@@ -122,6 +122,12 @@ struct apm_ctx {
     // iterations (APM_OVERLAP_K=0: after them, on the main stream)
     bool overlap_k = true;
     hipStream_t stream2 = nullptr;
+    // one-panel lookahead of the Newton factorisation (APM_LOOKAHEAD, chol_range32): the far part
+    // of each trailing update on stream3 beside the next panel's dataflow launch
+    bool lookahead = true;
+    hipStream_t stream3 = nullptr;
+    hipEvent_t ev_la[4] = {nullptr, nullptr, nullptr, nullptr};
+    int la_i = 0;
     hipEvent_t ev_gram = nullptr, ev_cholk = nullptr;
     hipEvent_t ev_feed[4] = {nullptr, nullptr, nullptr, nullptr};
     int feed_i = 0;
@@ -397,7 +403,8 @@ std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend
 }
 
 void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
-                      int count, int fuse_k = -1, int fail_code = 0) {
+                      int count, int fuse_k = -1, int fail_code = 0, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
     const auto tl = tile_list(c, i0, R, j0, jend, Gap{0, 0});
@@ -406,17 +413,17 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     if (fuse_k >= 0)
         fd = FusedDiag<float>{1, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, fail_code};
     const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
-    ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl);
-    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl);
+    ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl, st);
+    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl, st);
     if (kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
         // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a
         // row vector (rhs_row_update32)
         const int rhs = R > c->nb ? c->nb : -1;
         const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
-        launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, c->stream,
-                                  fd, c->h3_now ? c->nb : 0, c->h3ok, rhs);
+        launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
+                                  c->h3_now ? c->nb : 0, c->h3ok, rhs);
     } else {
-        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, c->stream, fd,
+        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, st, fd,
                              c->h3_now ? c->nb : 0, c->h3ok);
     }
     check_launch();
@@ -429,6 +436,8 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
     const unsigned long long fact = ++c->df_fact;
+    bool far_pending = false;  // a far update on stream3 not yet joined (lookahead)
+    hipEvent_t e_far = nullptr;
     for (int K = k0; K < k1; K += c->outer32) {
         const int Kend = std::min(K + c->outer32, k1);
         if (c->df32) {  // the same steps in one dataflow launch per outer panel (chol32.hip)
@@ -446,6 +455,29 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
             check_launch();
             c->ticket_base += (unsigned long long)tickets;
             have_diag = Kend < k1;
+            const int Knext = std::min(Kend + c->outer32, Cb);
+            if (c->lookahead && Knext < Cb) {
+                // one-panel lookahead: the next panel's columns first (narrow, with the fused
+                // diagonal tile), its dataflow launch next on this stream, and the rest of the
+                // trailing update (far: columns >= Knext) on stream3 beside it. The narrow update
+                // shares its tiles with the previous panel's far update, so it waits for that.
+                hipEvent_t e_df = c->ev_la[c->la_i++ & 3];
+                HIPC(hipEventRecord(e_df, c->stream));
+                if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
+                tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Knext, count,
+                                 have_diag ? Kend : -1, fail_code);
+                HIPC(hipStreamWaitEvent(c->stream3, e_df, 0));
+                tracked_update32(c, M, K, Kend - K, Knext, R, Knext, Cb, count, -1, fail_code,
+                                 c->stream3);
+                e_far = c->ev_la[c->la_i++ & 3];
+                HIPC(hipEventRecord(e_far, c->stream3));
+                far_pending = true;
+                continue;
+            }
+            if (far_pending) {  // (the previous far update shares these tiles)
+                HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
+                far_pending = false;
+            }
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                              fail_code);
             continue;
@@ -467,6 +499,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
         tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
                          fail_code);
     }
+    if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
 }
 
 void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
@@ -1114,6 +1147,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
     if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
@@ -1122,6 +1156,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPC(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
         HIPC(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, least));
+        HIPC(hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, least));
+        for (hipEvent_t& e : c->ev_la) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&c->ev_cholk, hipEventDisableTiming));
         for (hipEvent_t& e : c->ev_feed) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1229,7 +1265,11 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
 void free_ctx(apm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    // every stream drained before its buffers go (stream2 / stream3 work is joined into the main
+    // stream by every call, but a call that threw may have left some behind)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    if (c->stream3) (void)hipStreamSynchronize(c->stream3);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->hpin) (void)hipHostFree(c->hpin);
     if (c->hblk) (void)hipHostFree(c->hblk);
@@ -1237,7 +1277,9 @@ void free_ctx(apm_ctx* c) {
     if (c->hx) (void)hipHostFree(c->hx);
     if (c->hmask) (void)hipHostFree(c->hmask);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    if (c->stream3) (void)hipStreamDestroy(c->stream3);
+    for (hipEvent_t e : c->ev_la)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->ev_gram) (void)hipEventDestroy(c->ev_gram);

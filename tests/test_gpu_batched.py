@@ -224,8 +224,10 @@ def test_batched_mi_mh_consistent_and_batch_invariant(gpu_available):
     # the reference's default -1 adapts on the last count, the theta step (samplers.py:70, 143)
     ath, sc, rates = smp.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5)
     assert ath.shape == (4, 8, smp.P) and sc.shape == (4, 2, smp.P)
-    twin = S(X, y, 4, 16, prior, prop_scales=0.1, seed=61)
+    twin = S(X, y, 4, 16, prior, prop_scales=0.1, seed=61)  # the same calls, explicit index
     twin.get_samples(6, th0)
+    with pytest.raises(ValueError):  # (its first batch ran before the index was looked at)
+        twin.adaptive_run(th[:, -1], 3, 1, 0.15, 0.30, lambda b, n: 1.5, reject_count_index=0)
     ath1, sc1, rates1 = twin.adaptive_run(th[:, -1], 4, 2, 0.15, 0.30, lambda b, n: 1.5,
                                           reject_count_index=1)
     np.testing.assert_array_equal(rates1, rates)

@@ -3,5 +3,3 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r05c; mkdir -p $O
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-value -Wno-unused-result $1 -x hip tools/upd32_bench.cpp -o /tmp/upd32 || exit 1
 for K in 0 1 2 3 4 5 6; do timeout -k 5 60 /tmp/upd32 64 $K 10 || exit $?; done | tee $O/upd32$2.txt
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/hblt_bench.cpp -lhipblaslt -o /tmp/hblt || exit 1
-for K in 0 1 2 3 4 5 6; do timeout -k 5 120 /tmp/hblt 64 $K 10 || exit $?; done | tee $O/hblt$2.txt
