@@ -116,7 +116,8 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
-                               int hlim = 0, const int* h3ok = nullptr, int rhs = -1);
+                               int hlim = 0, const int* h3ok = nullptr, int rhs = -1,
+                               int role = 0);  // role 1: the posterior bottom block (a name only)
 // solo >= 0: row tile solo gets super-tile rows of its own (never paired with another row tile)
 std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
                                               int solo = -1);

@@ -850,7 +850,8 @@ void post_bottom32_steps(apm_ctx* c, int count, int K, int Kend, hipStream_t s) 
         c->prof ? update_flops(row0, 2 * nb, Kend, nb, Kend - K, Gap{0, 0}) * c->live_n : 0.0;
     ProfScope ps(c, APM_PROF_POST32_OUTER, fl, s);
     launch_chol_update32_t128(S, K, Kend - K, sl.first, sl.second, lv, count, s,
-                              FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, hlim, c->h3post);
+                              FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, hlim, c->h3post,
+                              -1, /*role: the posterior bottom block*/ 1);
     check_launch();
 }
 

@@ -23,12 +23,16 @@
 
 #define KS32 32          // slice depth (floats) of the LDS-staged tile GEMM
 #define LP32 (KS32 + 2)  // pitch 34 floats: fragment reads (16 rows x 4 k) hit 32 distinct banks
-// fp16x3 operands (see k_chol_update32_t128): hi and lo halves of a 32-deep slice, rows padded to
-// 40 halves (80 B: the 16-byte fragment reads of 8 row-consecutive lanes hit 8 distinct 16-byte
-// bank groups)
+// fp16x3 operands (see k_chol_update32_t128): hi and lo halves of a 32-deep slice, 64-byte rows
+// (four 16-byte pieces) with the piece index XOR-swizzled by bit 3 of the row (HS): the 16-byte
+// fragment reads of an MFMA (lane = row r16 + 16 x, piece kq) then hit 16 distinct bank quads in
+// every ds_read_b128 lane group, and the 8-byte stores of two consecutive rows fill the 32
+// banks of a ds_write_b64 group once (the round-4 80-byte pitch left 2-way read conflicts: 48 %
+// of the update's LDS cycles, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r05_pmc_newton.txt)
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-#define LPH 40
+#define LPH 32
+#define HS(r, c) (((((c) >> 3) ^ (((r) >> 2) & 2)) << 3) | ((c) & 7))
 struct GemmSmem32 {
     union {
         struct {
@@ -115,11 +119,11 @@ __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* _
             for (int h = 0; h < PPT; ++h) {
                 h4_t hi, lo;
                 split_h3(NEG ? -ra[h] : ra[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.ah[buf][prow[h]][pcol[h]]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.al[buf][prow[h]][pcol[h]]) = lo;
+                *reinterpret_cast<h4_t*>(&sm.ah[buf][prow[h]][HS(prow[h], pcol[h])]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.al[buf][prow[h]][HS(prow[h], pcol[h])]) = lo;
                 split_h3(rb[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.bh[buf][prow[h]][pcol[h]]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.bl[buf][prow[h]][pcol[h]]) = lo;
+                *reinterpret_cast<h4_t*>(&sm.bh[buf][prow[h]][HS(prow[h], pcol[h])]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.bl[buf][prow[h]][HS(prow[h], pcol[h])]) = lo;
             }
             return;
         }
@@ -136,10 +140,10 @@ __device__ __forceinline__ void tile_gemm_nt32(f4_t (&acc)[2][2], const float* _
             h8_t ah[2], al[2], bh[2], bl[2];
 #pragma unroll
             for (int x = 0; x < 2; ++x) {
-                ah[x] = *reinterpret_cast<const h8_t*>(&sm.ah[cur][32 * wr + 16 * x + r16][8 * kq]);
-                al[x] = *reinterpret_cast<const h8_t*>(&sm.al[cur][32 * wr + 16 * x + r16][8 * kq]);
-                bh[x] = *reinterpret_cast<const h8_t*>(&sm.bh[cur][32 * wc + 16 * x + r16][8 * kq]);
-                bl[x] = *reinterpret_cast<const h8_t*>(&sm.bl[cur][32 * wc + 16 * x + r16][8 * kq]);
+                ah[x] = *reinterpret_cast<const h8_t*>(&sm.ah[cur][32 * wr + 16 * x + r16][HS(32 * wr + 16 * x + r16, 8 * kq)]);
+                al[x] = *reinterpret_cast<const h8_t*>(&sm.al[cur][32 * wr + 16 * x + r16][HS(32 * wr + 16 * x + r16, 8 * kq)]);
+                bh[x] = *reinterpret_cast<const h8_t*>(&sm.bh[cur][32 * wc + 16 * x + r16][HS(32 * wc + 16 * x + r16, 8 * kq)]);
+                bl[x] = *reinterpret_cast<const h8_t*>(&sm.bl[cur][32 * wc + 16 * x + r16][HS(32 * wc + 16 * x + r16, 8 * kq)]);
             }
 #pragma unroll
             for (int bi = 0; bi < 2; ++bi)
@@ -733,7 +737,9 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
         }
     }
 }
-template <bool H3>
+// ROLE only names the instantiation (0: the Newton factorisation, 1: the posterior factor's
+// bottom block, postcov.hip): the two launch populations get separate rocprofv3 counter figures
+template <bool H3, int ROLE>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
@@ -826,11 +832,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
             for (int h = 0; h < 4; ++h) {
                 h4_t hi, lo;
                 split(ra[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.h.ah[buf][prow[h]][pcol[h]]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.h.al[buf][prow[h]][pcol[h]]) = lo;
+                *reinterpret_cast<h4_t*>(&sm.h.ah[buf][prow[h]][HS(prow[h], pcol[h])]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.h.al[buf][prow[h]][HS(prow[h], pcol[h])]) = lo;
                 split(rb[h], hi, lo);
-                *reinterpret_cast<h4_t*>(&sm.h.bh[buf][prow[h]][pcol[h]]) = hi;
-                *reinterpret_cast<h4_t*>(&sm.h.bl[buf][prow[h]][pcol[h]]) = lo;
+                *reinterpret_cast<h4_t*>(&sm.h.bh[buf][prow[h]][HS(prow[h], pcol[h])]) = hi;
+                *reinterpret_cast<h4_t*>(&sm.h.bl[buf][prow[h]][HS(prow[h], pcol[h])]) = lo;
             }
         };
         // lane (r16, kq): k = 8kq .. 8kq+7 of the slice = one 16-byte read per half and tile;
@@ -842,15 +848,15 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
             h8_t bh[4], bl[4];
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
-                bh[x] = *reinterpret_cast<const h8_t*>(&sm.h.bh[cur][64 * wc + 16 * x + r16][8 * kq]);
-                bl[x] = *reinterpret_cast<const h8_t*>(&sm.h.bl[cur][64 * wc + 16 * x + r16][8 * kq]);
+                bh[x] = *reinterpret_cast<const h8_t*>(&sm.h.bh[cur][64 * wc + 16 * x + r16][HS(64 * wc + 16 * x + r16, 8 * kq)]);
+                bl[x] = *reinterpret_cast<const h8_t*>(&sm.h.bl[cur][64 * wc + 16 * x + r16][HS(64 * wc + 16 * x + r16, 8 * kq)]);
             }
 #pragma unroll
             for (int bi = 0; bi < 4; ++bi) {
                 const h8_t ah =
-                    *reinterpret_cast<const h8_t*>(&sm.h.ah[cur][64 * wr + 16 * bi + r16][8 * kq]);
+                    *reinterpret_cast<const h8_t*>(&sm.h.ah[cur][64 * wr + 16 * bi + r16][HS(64 * wr + 16 * bi + r16, 8 * kq)]);
                 const h8_t al =
-                    *reinterpret_cast<const h8_t*>(&sm.h.al[cur][64 * wr + 16 * bi + r16][8 * kq]);
+                    *reinterpret_cast<const h8_t*>(&sm.h.al[cur][64 * wr + 16 * bi + r16][HS(64 * wr + 16 * bi + r16, 8 * kq)]);
 #pragma unroll
                 for (int bj = 0; bj < 4; ++bj) {
                     acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[bj], acc[bi][bj], 0, 0, 0);
@@ -980,15 +986,19 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
-                               int hlim, const int* h3ok, int rhs) {
+                               int hlim, const int* h3ok, int rhs, int role) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    if (hlim > 0)
-        hipLaunchKernelGGL(k_chol_update32_t128<true>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, hlim, h3ok, rhs);
-    else
-        hipLaunchKernelGGL(k_chol_update32_t128<false>, dim3((unsigned)total), dim3(256), 0, s, A,
-                           k0, kc, tiles, ntiles, nchains, live, fd, 0, nullptr, rhs);
+#define UPD32_LAUNCH(H, R)                                                                     \
+    hipLaunchKernelGGL((k_chol_update32_t128<H, R>), dim3((unsigned)total), dim3(256), 0, s, A, \
+                       k0, kc, tiles, ntiles, nchains, live, fd, H ? hlim : 0,               \
+                       H ? h3ok : nullptr, rhs)
+    if (hlim > 0) {
+        if (role) UPD32_LAUNCH(true, 1); else UPD32_LAUNCH(true, 0);
+    } else {
+        if (role) UPD32_LAUNCH(false, 1); else UPD32_LAUNCH(false, 0);
+    }
+#undef UPD32_LAUNCH
 }
 
 // Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),

@@ -853,16 +853,15 @@ def main():
                           'hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 accumulation; '
                           'achieved in fp32-equivalent flops against the fp16 peak / 3)',
                           PEAK_F16X3_TFLOPS,
-                          ('k_chol_update32_t128<true, false>', 'k_chol_update32_t128<true, true>',
-                           'k_chol_update32_t128<false, false>',  # round-2 names:
-                           'k_chol_update32_t128<true>', 'k_chol_update32_t128<false>'), 'f16x3')
-    # the posterior factor's fp32 bottom block (same kernel as the Newton update, so its PMC
-    # traffic cannot be told apart in a counter pass: timing and flops only)
+                          ('k_chol_update32_t128<true, 0>', 'k_chol_update32_t128<false, 0>'),
+                          'f16x3')
+    # the posterior factor's fp32 bottom block: the same kernel under its own instantiation name
+    # (ROLE = 1, chol32.hip), so its counter figures are its own
     post32 = mfma_roofline('post32', 'k_chol_update32_t128 on the posterior factor\'s bottom block '
                            '(L_K J) L\'^-T (fp32 / fp16x3, second stream; postcov.hip)',
-                           PEAK_F16X3_TFLOPS, (), 'f16x3')
-    if post32 is not None:
-        post32['traffic_note'] = 'shares its kernel with the Newton update: no separate PMC pass'
+                           PEAK_F16X3_TFLOPS,
+                           ('k_chol_update32_t128<true, 1>', 'k_chol_update32_t128<false, 1>'),
+                           'f16x3')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
     roofline = max(cands, key=lambda r: r['share_of_step_time'])
