@@ -90,13 +90,27 @@ struct SpinCtl {
     unsigned long long* timeouts;  // bounded-spin exits (APM_PROF_DF / _TRSV_TIMEOUTS)
     int limit;                     // polls before a wait gives up
 };
+// fp16x3 operand planes of one outer panel of the Newton matrix (chol32.hip): for each 32-column
+// slice s of the panel and row r < rows, hi = fp16(x) and lo = fp16(x - hi) of the row's 32
+// entries (64 bytes each), hi at base + b * cstride + (s * rows + r) * 32 and lo at + lo (fp16
+// bit patterns). Written by the dataflow panel kernel for the rows below the panel's diagonal
+// block; the trailing update then stages them into LDS with DMA instead of splitting fp32
+// operands in registers. base == nullptr: no planes.
+struct Planes16 {
+    unsigned short* base;
+    int64_t cstride;
+    int64_t lo;
+    int rows;
+};
 // tile columns [K, K+ncols) of an outer panel (diagonal tile (K, K) already factored) in one
 // dataflow launch (chol32.hip: per-(chain, row) progress words prog[b * pstride + row], monotonic
 // base per factorisation and panel); returns the launch's workgroup count (its tickets), 0 when
-// nothing was launched, -1 for a panel wider than the progress word allows
+// nothing was launched, -1 for a panel wider than the progress word allows. pl.base != nullptr:
+// the rows below the diagonal block (row tiles < pl.rows / 64) also write the panel's planes
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s);
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
+                            Planes16 pl = Planes16{nullptr, 0, 0, 0});
 // rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is final (fd.Dinv: its
 // inverses), each row a left-looking walk over the panel's columns with no waits; zrow > 0: row
 // tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)
@@ -117,7 +131,13 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
                                int hlim = 0, const int* h3ok = nullptr, int rhs = -1,
-                               int role = 0);  // role 1: the posterior bottom block (a name only)
+                               int role = 0,  // role 1: the posterior bottom block (a name only)
+                               Planes16 pl = Planes16{nullptr, 0, 0, 0});  // k0's panel's planes
+// the far trailing updates of the Newton factorisation on 256x256 quad tiles (chol32.hip): fp16x3
+// operands from the planes only, rows below the appended right-hand side, chains with h3ok set
+void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, int nq, Live live,
+                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl);
+std::vector<unsigned> build_update_quads(int i0, int R, int j0, int jend);
 // solo >= 0: row tile solo gets super-tile rows of its own (never paired with another row tile)
 std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
                                               int solo = -1);

@@ -94,9 +94,14 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> tile_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
+    std::map<std::tuple<int, int, int, int>, std::pair<unsigned*, int>> quad_lists;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     bool h3 = true;       // APM_H3=0: fp32 operands in the fp32 factorisations' outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
+    bool h3_all = false;  // ... and every chain may (the quad-tile far updates need that)
+    // far trailing updates of the Newton factorisation on 256x256 quad tiles (k_chol_update32_q256,
+    // needs the planes; APM_Q256=0: the 128-row super-tile kernel)
+    bool q256 = true;
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
     int* h3post = nullptr;  // the same for the posterior factor's fp32 bottom block (h3ok + B)
     // the bottom block of the posterior factor [[J M J],[L_K J]] (the TRSM that yields chol(C) J)
@@ -108,6 +113,13 @@ struct apm_ctx {
     // in-panel factorisation of the Newton matrix: one dataflow launch per outer panel
     // (k_chol_panel_df32; APM_DF32=0: the launch sequence it replaces)
     bool df32 = true;
+    // the dataflow launch also writes the panel's fp16x3 operand planes (Planes16), which the
+    // trailing update stages with LDS-DMA instead of splitting fp32 operands in registers (two
+    // buffers by panel parity: the lookahead's far update reads panel K's while the dataflow
+    // launch of K + 1 writes its own; APM_PLANES=0: split while staged)
+    bool planes_on = true;
+    unsigned short* planes = nullptr;
+    int64_t plane_cs = 0;  // halves per chain and buffer
     // per (chain, row tile) progress words, then [dataflow timeouts][TRSV timeouts][ticket]
     unsigned long long* dfprog = nullptr;
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
@@ -383,6 +395,11 @@ void trsv32(apm_ctx* c, bool fwd, MatF F, const float* D, int64_t ds, const doub
         spin_ctl(c, true), c->stream);
     check_launch();
 }
+Planes16 planes_of(apm_ctx* c, int K) {
+    if (!c->planes || !c->h3_now) return Planes16{nullptr, 0, 0, 0};
+    return Planes16{c->planes + ((K / c->outer32) & 1) * c->max_batch * c->plane_cs, c->plane_cs,
+                    c->plane_cs / 2, c->np};
+}
 MatF b32_of(apm_ctx* c) {
     return MatF{reinterpret_cast<float*>(c->A.base), c->np, 2 * c->A.cstride};
 }
@@ -402,8 +419,22 @@ std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend
     return val;
 }
 
+std::pair<unsigned*, int> quad_list(apm_ctx* c, int i0, int R, int j0, int jend) {
+    auto key = std::make_tuple(i0, R, j0, jend);
+    auto it = c->quad_lists.find(key);
+    if (it != c->quad_lists.end()) return it->second;
+    std::vector<unsigned> v = build_update_quads(i0, R, j0, jend);
+    unsigned* d = dalloc<unsigned>(c, std::max<size_t>(1, v.size()));
+    if (!v.empty())
+        HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
+    auto val = std::make_pair(d, (int)v.size());
+    c->quad_lists[key] = val;
+    return val;
+}
+
 void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
-                      int count, int fuse_k = -1, int fail_code = 0, hipStream_t st = nullptr) {
+                      int count, int fuse_k = -1, int fail_code = 0, hipStream_t st = nullptr,
+                      Planes16 pl = Planes16{nullptr, 0, 0, 0}) {
     if (!st) st = c->stream;
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
@@ -419,9 +450,22 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
         // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a
         // row vector (rhs_row_update32)
         const int rhs = R > c->nb ? c->nb : -1;
-        const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
-        launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
-                                  c->h3_now ? c->nb : 0, c->h3ok, rhs);
+        if (pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb) {
+            // rows above the right-hand side on quad tiles, that row on the 128-row kernel
+            const auto ql = quad_list(c, i0, std::min(R, c->nb), j0, jend);
+            launch_chol_update32_q256(M, k0, kc, ql.first, ql.second, live_of(c), count, st,
+                                      c->h3ok, pl);
+            if (rhs >= 0) {
+                check_launch();
+                const auto sl = super_list(c, c->nb, R, j0, jend, Gap{0, 0}, rhs);
+                launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st,
+                                          fd, c->nb, c->h3ok, rhs, 0, pl);
+            }
+        } else {
+            const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
+            launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
+                                      c->h3_now ? c->nb : 0, c->h3ok, rhs, 0, pl);
+        }
     } else {
         launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, st, fd,
                              c->h3_now ? c->nb : 0, c->h3ok);
@@ -450,7 +494,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                 M, K, Kend - K, R, FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
                 count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
                 (fact << 16) | ((unsigned long long)(K / c->outer32) << 4), spin_ctl(c, false),
-                c->stream);
+                c->stream, planes_of(c, K));
             if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
             c->ticket_base += (unsigned long long)tickets;
@@ -465,10 +509,10 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                 HIPC(hipEventRecord(e_df, c->stream));
                 if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
                 tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Knext, count,
-                                 have_diag ? Kend : -1, fail_code);
+                                 have_diag ? Kend : -1, fail_code, nullptr, planes_of(c, K));
                 HIPC(hipStreamWaitEvent(c->stream3, e_df, 0));
                 tracked_update32(c, M, K, Kend - K, Knext, R, Knext, Cb, count, -1, fail_code,
-                                 c->stream3);
+                                 c->stream3, planes_of(c, K));
                 e_far = c->ev_la[c->la_i++ & 3];
                 HIPC(hipEventRecord(e_far, c->stream3));
                 far_pending = true;
@@ -479,7 +523,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                 far_pending = false;
             }
             tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
-                             fail_code);
+                             fail_code, nullptr, planes_of(c, K));
             continue;
         }
         // APM_DF32=0: the launch sequence the dataflow kernel replaces (left-looking inside the
@@ -552,7 +596,11 @@ int* pin_h3post(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 20 * c->ma
 void upload_h3(apm_ctx* c, int count) {
     int* h = pin_h3(c);
     c->h3_now = false;
-    for (int b = 0; b < count; ++b) c->h3_now |= h[b] != 0;
+    c->h3_all = count > 0;
+    for (int b = 0; b < count; ++b) {
+        c->h3_now |= h[b] != 0;
+        c->h3_all &= h[b] != 0;
+    }
     HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->h3post, pin_h3post(c), sizeof(int) * count, hipMemcpyHostToDevice,
                         c->stream));
@@ -1149,6 +1197,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
     if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
+    if (const char* e = getenv("APM_PLANES")) c->planes_on = atoi(e) != 0;
+    if (const char* e = getenv("APM_Q256")) c->q256 = atoi(e) != 0;
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
@@ -1228,6 +1278,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->h3post = c->h3ok + B;
     // + 3: the bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS) and of the
     // TRSV (APM_PROF_TRSV_TIMEOUTS), the arrival-ticket counter (spin_words)
+    if (c->mixed && c->df32 && c->h3 && c->planes_on) {
+        c->plane_cs = 2 * np * 32 * 2 * c->outer32;  // 2 planes x rows x 2 outer32 slices x 32
+        c->planes = dalloc<unsigned short>(c, 2 * B * c->plane_cs);
+    }
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 3);
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 3)));
     // one block of 7B words, mirrored in pinned host memory and uploaded with one copy:

@@ -388,7 +388,7 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          unsigned long long* prog,
                                                          int64_t pstride,
                                                          unsigned long long base, SpinCtl sc,
-                                                         int row0 = 0, int zrow = 0) {
+                                                         Planes16 pl, int row0 = 0, int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -623,6 +623,24 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
             DF_STAMP(4);
         } else {
             tile32_store(x, Aik, A.ld, wr, wc, lane);
+            if (!BULK && pl.base && (i + 1) * 64 <= pl.rows) {
+                // the trailing update's fp16x3 operand planes: this wave's 32x32 block is rows
+                // 32wr .. +31 of slice 2(k - K) + wc (Planes16)
+                unsigned short* hp = pl.base + b * pl.cstride +
+                                     ((int64_t)(2 * c + wc) * pl.rows + i * 64 + 32 * wr) * 32;
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float v = x[bi][bj][r];
+                            const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
+                            const int o = (16 * bi + F32_CROW(lane, r)) * 32 + 16 * bj + (lane & 15);
+                            hp[o] = __builtin_bit_cast(unsigned short, h);
+                            hp[pl.lo + o] = __builtin_bit_cast(unsigned short, l);
+                        }
+            }
             __syncthreads();  // the staging area is reused by the next column's update
         }
     }
@@ -630,14 +648,15 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
 
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
-                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s) {
+                            int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
+                            Planes16 pl) {
     // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
     // caller raises) instead of being left unfactored
     if (ncols > 14) return -1;
     if (ncols < 1 || R - K <= 1) return 0;  // (one column: its panel TRSM)
     const long grid = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
-                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc);
+                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc, pl);
     return grid;
 }
 
@@ -647,7 +666,8 @@ void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zro
     if (ncols < 1 || R <= row0) return;
     hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
-                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0}, row0, zrow);
+                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0},
+                       Planes16{nullptr, 0, 0, 0}, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -737,15 +757,17 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
         }
     }
 }
-// ROLE only names the instantiation (0: the Newton factorisation, 1: the posterior factor's
-// bottom block, postcov.hip): the two launch populations get separate rocprofv3 counter figures
+// ROLE 0: the Newton factorisation, 1: the posterior factor's bottom block (postcov.hip; the same
+// code, a separate instantiation so that the two launch populations get separate rocprofv3
+// counter figures), 2: the Newton factorisation with the fp16x3 operands read from the dataflow
+// kernel's planes (Planes16) instead of split while staged
 template <bool H3, int ROLE>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
                                                                int ntiles, int nchains, Live live,
                                                                FusedDiag<float> fd, int hlim,
                                                                const int* __restrict__ h3ok,
-                                                               int rhs) {
+                                                               int rhs, Planes16 pl) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
     const int r16 = lane & 15, kq = lane >> 4;
     __shared__ union {
@@ -785,16 +807,77 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
     const int nsub = (64 * kc) / KS128;
     const int li = mine ? oi : (wr ? ra1 : ra0), lj = mine ? oj : (wc ? cb1 : cb0);
     const float* Cw = Ab + (int64_t)(li * 64) * A.ld + lj * 64;
+    auto load_old = [&]() {
 #pragma unroll
-    for (int bi = 0; bi < 4; ++bi)
+        for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
+            for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                acc[bi][bj][r] = -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
+                for (int r = 0; r < 4; ++r)
+                    acc[bi][bj][r] =
+                        -Cw[(int64_t)(16 * bi + F32_CROW(lane, r)) * A.ld + 16 * bj + r16];
+    };
     // super-tile rows below hlim (the appended right-hand side row), chains flagged in h3ok
     const bool use_h3 = H3 && ti + (rv1 ? 1 : 0) < hlim && (!h3ok || h3ok[b]);
-    if (use_h3) {
+    if (!(ROLE == 2 && use_h3)) load_old();
+    if (ROLE == 2 && use_h3) {
+        // operands already split by the dataflow panel kernel (Planes16): LDS-DMA staging, no
+        // registers, no VALU. Wave wv fills one array (0: A hi, 1: A lo, 2: B hi, 3: B lo) of a
+        // slice, 8 global_load_lds_dwordx4 of 16 rows x 64 B; lane l takes row 16q + l/4 and
+        // stores LDS slot l%4, i.e. logical piece (l%4) ^ (bit 3 of the row) - the HS layout that
+        // compute() reads
+        const int rowl = lane >> 2, piece = (lane & 3) ^ ((rowl >> 2) & 2);
+        const int t0 = wv < 2 ? ra0 : cb0, t1 = wv < 2 ? ra1 : cb1;
+        const unsigned short* P = pl.base + b * pl.cstride + ((wv & 1) ? pl.lo : 0) +
+                                  (int64_t)rowl * 32 + piece * 8;
+        const unsigned short* p0 = P + (int64_t)t0 * 64 * 32;
+        const unsigned short* p1 = P + (int64_t)t1 * 64 * 32;
+        const int64_t sstep = (int64_t)pl.rows * 32;
+        _Float16* lbase = &sm.h.ah[0][0][0] + wv * (2 * 128 * LPH);
+        auto dma = [&](int sidx, int buf) {
+            const int64_t o = sidx * sstep;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                __builtin_amdgcn_global_load_lds(
+                    (glb_void_t*)((q < 4 ? p0 : p1) + o + (16 * (q & 3)) * 32),
+                    (lds_void_t*)(lbase + (buf * 128 + 16 * q) * LPH), 16, 0, 0);
+        };
+        auto compute = [&](int cur) {
+            h8_t bh[4], bl[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                bh[x] = *reinterpret_cast<const h8_t*>(&sm.h.bh[cur][64 * wc + 16 * x + r16][HS(64 * wc + 16 * x + r16, 8 * kq)]);
+                bl[x] = *reinterpret_cast<const h8_t*>(&sm.h.bl[cur][64 * wc + 16 * x + r16][HS(64 * wc + 16 * x + r16, 8 * kq)]);
+            }
+#pragma unroll
+            for (int bi = 0; bi < 4; ++bi) {
+                const h8_t ah =
+                    *reinterpret_cast<const h8_t*>(&sm.h.ah[cur][64 * wr + 16 * bi + r16][HS(64 * wr + 16 * bi + r16, 8 * kq)]);
+                const h8_t al =
+                    *reinterpret_cast<const h8_t*>(&sm.h.al[cur][64 * wr + 16 * bi + r16][HS(64 * wr + 16 * bi + r16, 8 * kq)]);
+#pragma unroll
+                for (int bj = 0; bj < 4; ++bj) {
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[bj], acc[bi][bj], 0, 0, 0);
+                    acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[bj], acc[bi][bj], 0, 0, 0);
+                }
+            }
+        };
+        dma(0, 0);
+        load_old();  // while the first slice is in flight
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj) asm volatile("" : "+v"(acc[bi][bj]));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int s = 0; s < nsub; ++s) {
+            if (s + 1 < nsub) dma(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
+            if (mine) compute(s & 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else if (ROLE != 2 && use_h3) {
         // register staging: thread tid moves 16-byte pieces p = tid + 256h (row p/8, k 4(p%8))
         // of both operands
         const float* arow[4];
@@ -986,19 +1069,177 @@ __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, i
 
 void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, int ntiles,
                                Live live, int nchains, hipStream_t s, FusedDiag<float> fd,
-                               int hlim, const int* h3ok, int rhs, int role) {
+                               int hlim, const int* h3ok, int rhs, int role, Planes16 pl) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
 #define UPD32_LAUNCH(H, R)                                                                     \
     hipLaunchKernelGGL((k_chol_update32_t128<H, R>), dim3((unsigned)total), dim3(256), 0, s, A, \
                        k0, kc, tiles, ntiles, nchains, live, fd, H ? hlim : 0,               \
-                       H ? h3ok : nullptr, rhs)
+                       H ? h3ok : nullptr, rhs, pl)
     if (hlim > 0) {
-        if (role) UPD32_LAUNCH(true, 1); else UPD32_LAUNCH(true, 0);
+        if (pl.base) UPD32_LAUNCH(true, 2);
+        else if (role) UPD32_LAUNCH(true, 1);
+        else UPD32_LAUNCH(true, 0);
     } else {
         if (role) UPD32_LAUNCH(false, 1); else UPD32_LAUNCH(false, 0);
     }
 #undef UPD32_LAUNCH
+}
+
+// ------------------------------------------------------------------------- 256x256 trailing update
+// The Newton factorisation's far trailing updates with fp16x3 operands from the dataflow kernel's
+// planes (Planes16): one 256x256 quad tile (4x4 tiles) per workgroup of 8 waves (2 x 4), each wave
+// a 128x64 block (8x4 accumulators of v_mfma_f32_16x16x32_f16, three products per block as in
+// k_chol_update32_t128). Per 32-deep slice a wave issues 96 MFMAs (1536 cycles) against 24 fragment
+// reads; the operands of the next slice arrive by LDS-DMA (global_load_lds_dwordx4, 8 per wave)
+// while the slice is multiplied: the 128-row super-tile's 48 MFMAs per slice and barrier left the
+// loop waiting on its loads (29 % MFMA busy at 0.1 % LDS bank conflicts, profiles/
+// r05_pmc_newton_swizzled.txt). 128 KB of LDS: one workgroup per CU, two waves per SIMD.
+// Quad entries (build_update_quads): (I << 20) | (J << 8) | rmask << 4 | cmask, row tiles I .. I+3
+// and column tiles J .. J+3 with per-tile validity; tile (I+a, J+c) is written iff rmask bit a,
+// cmask bit c and J+c <= I+a. Invalid row/column tiles read tile I / J (no out-of-range reads;
+// their results are dropped). Only chains with fp16x3 operands and rows below the appended
+// right-hand side (the caller launches k_chol_update32_t128 for that row and for any batch with
+// a chain outside fp16's range). Same slices in the same order as k_chol_update32_t128, so the
+// tiles are bitwise those of the 128-row kernel.
+struct __attribute__((aligned(16))) GemmSmemQ {
+    _Float16 q[2][4][256][LPH];  // [buffer][A hi, A lo, B hi, B lo][row][k] (HS layout)
+};
+__global__ __launch_bounds__(512, 1) void k_chol_update32_q256(MatF A, int k0, int kc,
+                                                               const unsigned* __restrict__ quads,
+                                                               int nq, int nchains, Live live,
+                                                               const int* __restrict__ h3ok,
+                                                               Planes16 pl) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 2, wc = wv & 3;
+    const int r16 = lane & 15, kq = lane >> 4;
+    __shared__ GemmSmemQ sm;
+    const long w = xcd_remap32((long)blockIdx.x, (long)nq * nchains);
+    const int b = (int)(w / nq), t = (int)(w % nq);
+    if (!live32(live, b) || (h3ok && !h3ok[b])) return;
+    const unsigned e = quads[t];
+    const int I = (int)(e >> 20), J = (int)((e >> 8) & 0xfff), rm = (e >> 4) & 15, cm = e & 15;
+    auto rt = [&](int a) { return (rm >> a) & 1 ? I + a : I; };
+    auto ct = [&](int c) { return (cm >> c) & 1 ? J + c : J; };
+    // this wave's two 64x64 output tiles: rows I + 2wr + {0, 1}, column J + wc
+    const int oi0 = I + 2 * wr, oj = J + wc;
+    const bool v0 = ((rm >> (2 * wr)) & 1) && ((cm >> wc) & 1) && oj <= oi0;
+    const bool v1 = ((rm >> (2 * wr + 1)) & 1) && ((cm >> wc) & 1) && oj <= oi0 + 1;
+    float* Ab = A.base + b * A.cstride;
+    f4_t acc[8][4];
+    // LDS-DMA staging: wave wv fills rows 128 (wv & 1) .. +127 of array wv >> 1 (0: A hi, 1: A lo,
+    // 2: B hi, 3: B lo); lane l takes row 16q + l/4 and LDS slot l%4 = logical piece
+    // (l%4) ^ (bit 3 of the row) (the HS layout compute() reads)
+    const int arr = wv >> 1, half = wv & 1;
+    const int rowl = lane >> 2, piece = (lane & 3) ^ ((rowl >> 2) & 2);
+    const int ta = arr < 2 ? rt(2 * half) : ct(2 * half);
+    const int tb = arr < 2 ? rt(2 * half + 1) : ct(2 * half + 1);
+    const unsigned short* P = pl.base + b * pl.cstride + ((arr & 1) ? pl.lo : 0) +
+                              (int64_t)rowl * 32 + piece * 8;
+    const unsigned short* p0 = P + (int64_t)ta * 64 * 32;
+    const unsigned short* p1 = P + (int64_t)tb * 64 * 32;
+    const int64_t sstep = (int64_t)pl.rows * 32;
+    _Float16* lbase = &sm.q[0][arr][128 * half][0];
+    auto dma = [&](int sidx, int buf) {
+        const int64_t o = sidx * sstep;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_global_load_lds(
+                (glb_void_t*)((q < 4 ? p0 : p1) + o + (16 * (q & 3)) * 32),
+                (lds_void_t*)(lbase + (buf * 4 * 256 + 16 * q) * LPH), 16, 0, 0);
+    };
+    auto compute = [&](int cur) {
+        h8_t bh[4], bl[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const int row = 64 * wc + 16 * x + r16;
+            bh[x] = *reinterpret_cast<const h8_t*>(&sm.q[cur][2][row][HS(row, 8 * kq)]);
+            bl[x] = *reinterpret_cast<const h8_t*>(&sm.q[cur][3][row][HS(row, 8 * kq)]);
+        }
+#pragma unroll
+        for (int bi = 0; bi < 8; ++bi) {
+            if (!(bi < 4 ? v0 : v1)) continue;
+            const int row = 128 * wr + 16 * bi + r16;
+            const h8_t ah = *reinterpret_cast<const h8_t*>(&sm.q[cur][0][row][HS(row, 8 * kq)]);
+            const h8_t al = *reinterpret_cast<const h8_t*>(&sm.q[cur][1][row][HS(row, 8 * kq)]);
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj) {
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[bj], acc[bi][bj], 0, 0, 0);
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[bj], acc[bi][bj], 0, 0, 0);
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[bj], acc[bi][bj], 0, 0, 0);
+            }
+        }
+    };
+    const bool mine = v0 || v1;
+    const int nsub = (64 * kc) / KS128;
+    dma(0, 0);
+    // the old tiles, loaded while the first slice is in flight (a dropped tile reads tile (I, J)
+    // instead: unconditional loads, since a per-element load-or-not makes hipcc wait for each
+    // load in turn)
+#pragma unroll
+    for (int bi = 0; bi < 8; ++bi) {
+        const bool v = bi < 4 ? v0 : v1;
+        const float* Cw = Ab + (int64_t)((v ? oi0 + (bi >> 2) : I) * 64 + 16 * (bi & 3)) * A.ld +
+                          (v ? oj : J) * 64;
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[bi][bj][r] = -Cw[(int64_t)F32_CROW(lane, r) * A.ld + 16 * bj + r16];
+    }
+#pragma unroll
+    for (int bi = 0; bi < 8; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) asm volatile("" : "+v"(acc[bi][bj]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nsub; ++s) {
+        if (s + 1 < nsub) dma(s + 1, (s + 1) & 1);  // lands while slice s is multiplied
+        if (mine) compute(s & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int bi = 0; bi < 8; ++bi) {
+        if (!(bi < 4 ? v0 : v1)) continue;
+        float* Cw = Ab + (int64_t)((oi0 + (bi >> 2)) * 64 + 16 * (bi & 3)) * A.ld + oj * 64;
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                Cw[(int64_t)F32_CROW(lane, r) * A.ld + 16 * bj + r16] = -acc[bi][bj][r];
+    }
+}
+
+void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, int nq, Live live,
+                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl) {
+    if (nq <= 0 || !pl.base) return;
+    hipLaunchKernelGGL(k_chol_update32_q256, dim3((unsigned)((long)nq * nchains)), dim3(512), 0, s,
+                       A, k0, kc, quads, nq, nchains, live, h3ok, pl);
+}
+
+// Host: 256x256 quad tiles covering tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in
+// 2x2-quad blocks (8x8 tiles, the L2 locality of build_update_supertiles)
+std::vector<unsigned> build_update_quads(int i0, int R, int j0, int jend) {
+    std::vector<unsigned> v;
+    const int nr = (R - i0 + 3) / 4, nc = (jend - j0 + 3) / 4, S = 2;
+    for (int P = 0; P < nr; P += S)
+        for (int Q = 0; Q < nc; Q += S)
+            for (int p = P; p < std::min(P + S, nr); ++p)
+                for (int q = Q; q < std::min(Q + S, nc); ++q) {
+                    const int I = i0 + 4 * p, Jq = j0 + 4 * q;
+                    unsigned rm = 0, cm = 0;
+                    for (int a = 0; a < 4; ++a) {
+                        if (I + a < R) rm |= 1u << a;
+                        if (Jq + a < jend) cm |= 1u << a;
+                    }
+                    bool any = false;
+                    for (int a = 0; a < 4; ++a)
+                        for (int c = 0; c < 4; ++c)
+                            any |= ((rm >> a) & 1) && ((cm >> c) & 1) && Jq + c <= I + a;
+                    if (!any) continue;
+                    v.push_back(((unsigned)I << 20) | ((unsigned)Jq << 8) | (rm << 4) | cm);
+                }
+    return v;
 }
 
 // Host: 128x128 super-tiles covering tiles (i, j), i in [i0, R) minus the row gap [glo, ghi),

@@ -372,6 +372,38 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
         assert ob1[b] == o1[b]
 
 
+@pytest.mark.parametrize('n', [2048, 1700])
+def test_update_operand_planes_bitwise(nat, monkeypatch, n):
+    """The Newton factorisation's trailing updates stage fp16x3 operand planes that the dataflow
+    panel kernel writes (chol32.hip Planes16; the far updates on 256x256 quad tiles,
+    k_chol_update32_q256) instead of splitting fp32 operands while staging them (APM_PLANES=0),
+    or run on the 128-row kernel only (APM_Q256=0): the same split of the same values and the
+    same MFMA sequence per tile, so outputs, modes and iteration counts are bitwise equal.
+    n = 1700: ragged quad tiles (row and column masks). With a chain at theta_0 = 19.5 in the
+    batch (fp32 operands) the quad path falls back to the 128-row kernel for the whole call,
+    again bitwise."""
+    X, y, thetas, ns = _mixed_case(n=n)
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_PLANES=0)
+    assert (s0 == 0).all()
+    for env in ({}, {'APM_Q256': 0}):
+        o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, **env)
+        np.testing.assert_array_equal(s1, s0)
+        np.testing.assert_array_equal(n1, n0)
+        np.testing.assert_array_equal(o1, o0)
+        for b in range(len(thetas)):
+            np.testing.assert_array_equal(f1[b], f0[b])
+    big = thetas.copy()
+    big[2, 0] = 19.5
+    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_PLANES=0)
+    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch)
+    np.testing.assert_array_equal(sb1, sb0)
+    np.testing.assert_array_equal(nb1, nb0)
+    np.testing.assert_array_equal(ob1, ob0)
+    for b in range(len(big)):
+        if sb0[b] == 0:  # (a failed chain's slot is not written)
+            np.testing.assert_array_equal(fb1[b], fb0[b])
+
+
 def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
     """_run_is plus the slots' factors and the fp64-rerun counter of the posterior bottom block."""
     for k, v in env.items():

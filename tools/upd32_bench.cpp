@@ -12,6 +12,21 @@
 #include <vector>
 #pragma clang diagnostic ignored "-Wunused-result"
 
+// the fp16x3 planes of panel columns [k0*64, k0*64 + 64kc) of rows < np (Planes16 layout)
+__global__ void k_fill_planes(const float* A, int64_t ld, int64_t cs, int np, int k0, int kc,
+                              Planes16 pl) {
+    const int64_t n = (int64_t)np * 64 * kc;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (e >= n) return;
+    const int r = (int)(e / (64 * kc)), col = (int)(e % (64 * kc));
+    const float v = A[b * cs + (int64_t)r * ld + k0 * 64 + col];
+    const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
+    const int64_t o = b * pl.cstride + ((int64_t)(col >> 5) * pl.rows + r) * 32 + (col & 31);
+    pl.base[o] = __builtin_bit_cast(unsigned short, h);
+    pl.base[o + pl.lo] = __builtin_bit_cast(unsigned short, l);
+}
+
 static double upd_flops(int i0, int R, int j0, int jend, int kc) {
     double f = 0.0;
     for (int i = i0; i < R; ++i)
@@ -60,12 +75,44 @@ int main(int argc, char** argv) {
     const MatF M{A, ld, cs};
     const Live lv{act, st};
     const FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
+    // UPD_PLANES=1: operands from fp16x3 planes (filled from the pristine matrix before each
+    // checked launch; the timed launches reuse them) - the checksum must equal the split path's
+    Planes16 pl{nullptr, 0, 0, 0};
+    const char* pe = getenv("UPD_PLANES");
+    if (pe && atoi(pe)) {
+        const int64_t pcs = (int64_t)2 * np * 64 * kc;
+        hipMalloc(&pl.base, sizeof(unsigned short) * pcs * chains);
+        pl = Planes16{pl.base, pcs, pcs / 2, np};
+    }
+    auto fill = [&]() {
+        if (!pl.base) return;
+        hipLaunchKernelGGL(k_fill_planes, dim3((unsigned)(((int64_t)np * 64 * kc + 255) / 256), chains),
+                           dim3(256), 0, 0, A0, ld, cs, np, k0, kc, pl);
+    };
+    // UPD_Q256=1 (with UPD_PLANES=1): 256x256 quad tiles for the rows above the right-hand side,
+    // the 128-row kernel for that row alone
+    const char* qe = getenv("UPD_Q256");
+    const bool q256 = qe && atoi(qe) && pl.base;
+    std::vector<unsigned> ql = build_update_quads(Kend, nb, Kend, nb);
+    std::vector<unsigned> rl = build_update_supertiles(nb, R, Kend, nb, 0, 0, rhs);
+    unsigned *dql, *drl;
+    hipMalloc(&dql, sizeof(unsigned) * ql.size());
+    hipMemcpy(dql, ql.data(), sizeof(unsigned) * ql.size(), hipMemcpyHostToDevice);
+    hipMalloc(&drl, sizeof(unsigned) * rl.size());
+    hipMemcpy(drl, rl.data(), sizeof(unsigned) * rl.size(), hipMemcpyHostToDevice);
     auto launch = [&]() {
-        launch_chol_update32_t128(M, k0, kc, dsl, (int)sl.size(), lv, chains, nullptr, fd, nb, h3,
-                                  rhs);
+        if (q256) {
+            launch_chol_update32_q256(M, k0, kc, dql, (int)ql.size(), lv, chains, nullptr, h3, pl);
+            launch_chol_update32_t128(M, k0, kc, drl, (int)rl.size(), lv, chains, nullptr, fd, nb,
+                                      h3, rhs, 0, pl);
+        } else {
+            launch_chol_update32_t128(M, k0, kc, dsl, (int)sl.size(), lv, chains, nullptr, fd, nb,
+                                      h3, rhs, 0, pl);
+        }
     };
     // checksum of one launch from the pristine matrix
     hipMemcpy(A, A0, sizeof(float) * cs * chains, hipMemcpyDeviceToDevice);
+    fill();
     launch();
     hipDeviceSynchronize();
     std::vector<float> out((size_t)cs);
@@ -112,7 +159,7 @@ int main(int argc, char** argv) {
     float ms = 0.f;
     hipEventElapsedTime(&ms, e0, e1);
     const double fl = upd_flops(Kend, R - 1, Kend, nb, kc) * chains;  // (rhs row: not credited)
-    printf("K=%d chains=%d supertiles=%zu: %.4f ms/launch  %.1f TFLOP/s fp32-eq  sum %.9e hash "
-           "%016llx\n", K, chains, sl.size(), ms / reps, fl / (ms / reps * 1e-3) / 1e12, sum, hsh);
+    printf("%sK=%d chains=%d supertiles=%zu: %.4f ms/launch  %.1f TFLOP/s fp32-eq  sum %.9e hash "
+           "%016llx\n", q256 ? "q256 " : pl.base ? "planes " : "", K, chains, sl.size(), ms / reps, fl / (ms / reps * 1e-3) / 1e12, sum, hsh);
     return 0;
 }
