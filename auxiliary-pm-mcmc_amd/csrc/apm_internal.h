@@ -110,7 +110,16 @@ struct Planes16 {
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
-                            Planes16 pl = Planes16{nullptr, 0, 0, 0});
+                            Planes16 pl = Planes16{nullptr, 0, 0, 0}, int rhs_as = -1,
+                            bool inv_skip = false);
+// explicit-inverse panel of the Newton factorisation (chol32.hip), after a dataflow launch over
+// the diagonal block [K, K+8) and the right-hand-side row (rhs_as): Z = inv(L_D) of the 512x512
+// diagonal block as fp16x3 planes (zpl, 512 rows), with ZT = Z^T in fp32 scratch (zt: 512 x 512
+// per chain, zstride floats apart); then every row tile i in [K+8, nb) of the panel becomes
+// X_i = A_i Z^T in one fp16x3 GEMM (in place, plus the panel's planes pl). Chains with h3ok only.
+void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
+                        int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
+                        const int* h3ok, hipStream_t s);
 // rows [row0, R) of an outer panel [K, K+ncols) whose diagonal block is final (fd.Dinv: its
 // inverses), each row a left-looking walk over the panel's columns with no waits; zrow > 0: row
 // tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)

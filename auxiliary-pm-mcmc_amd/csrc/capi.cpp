@@ -120,6 +120,12 @@ struct apm_ctx {
     bool planes_on = true;
     unsigned short* planes = nullptr;
     int64_t plane_cs = 0;  // halves per chain and buffer
+    // explicit-inverse panels (APM_DFINV, chol32.hip k_panel_zt32 / k_panel_inv_gemm32): the
+    // dataflow launch walks the diagonal block and the right-hand-side row only; Z = inv(L_D) per
+    // chain (fp32 transposed scratch zt, fp16x3 planes zplanes) and one GEMM per row tile below
+    bool dfinv = true;
+    float* zt = nullptr;
+    unsigned short* zplanes = nullptr;
     // per (chain, row tile) progress words, then [dataflow timeouts][TRSV timeouts][ticket]
     unsigned long long* dfprog = nullptr;
     unsigned long long df_fact = 0;        // factorisations so far (the words' monotonic base)
@@ -490,14 +496,28 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                                    c->stream);
                 check_launch();
             }
+            // explicit-inverse panel for the fp16x3 chains; with every chain fp16x3 the dataflow
+            // launch covers the diagonal block and the right-hand-side row only, else all rows,
+            // those of the fp16x3 chains below the diagonal block returning at once
+            const bool inv = c->dfinv && c->zt && Kend - K == 8 && Kend < c->nb &&
+                             R <= c->nb + 1 && planes_of(c, K).base;
+            const bool compact = inv && c->h3_all;
             const long tickets = launch_chol_panel_df32(
-                M, K, Kend - K, R, FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv,
-                count, c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
+                M, K, Kend - K, compact ? Kend + (R > c->nb ? 1 : 0) : R,
+                FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv, count,
+                c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
                 (fact << 16) | ((unsigned long long)(K / c->outer32) << 4), spin_ctl(c, false),
-                c->stream, planes_of(c, K));
+                c->stream, planes_of(c, K), compact && R > c->nb ? c->nb : -1, inv && !compact);
             if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
             check_launch();
             c->ticket_base += (unsigned long long)tickets;
+            if (inv) {  // the rows below the diagonal block: X_i = A_i inv(L_D)^T
+                const int64_t zcs = 2 * 16 * 512 * 32;
+                launch_panel_inv32(M, K, c->nb, D, ds, c->zt, 512 * 512,
+                                   Planes16{c->zplanes, zcs, zcs / 2, 512}, planes_of(c, K), lv,
+                                   count, c->h3ok, c->stream);
+                check_launch();
+            }
             have_diag = Kend < k1;
             const int Knext = std::min(Kend + c->outer32, Cb);
             if (c->lookahead && Knext < Cb) {
@@ -1199,6 +1219,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
     if (const char* e = getenv("APM_PLANES")) c->planes_on = atoi(e) != 0;
     if (const char* e = getenv("APM_Q256")) c->q256 = atoi(e) != 0;
+    if (const char* e = getenv("APM_DFINV")) c->dfinv = atoi(e) != 0;
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
@@ -1281,6 +1302,10 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (c->mixed && c->df32 && c->h3 && c->planes_on) {
         c->plane_cs = 2 * np * 32 * 2 * c->outer32;  // 2 planes x rows x 2 outer32 slices x 32
         c->planes = dalloc<unsigned short>(c, 2 * B * c->plane_cs);
+        if (c->dfinv && c->outer32 == 8) {
+            c->zt = dalloc<float>(c, B * 512 * 512);
+            c->zplanes = dalloc<unsigned short>(c, B * 2 * 16 * 512 * 32);
+        }
     }
     c->dfprog = dalloc<unsigned long long>(c, (size_t)B * (c->nb + 1) + 3);
     HIPC(hipMemset(c->dfprog, 0, sizeof(unsigned long long) * (B * (c->nb + 1) + 3)));

@@ -388,7 +388,9 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          unsigned long long* prog,
                                                          int64_t pstride,
                                                          unsigned long long base, SpinCtl sc,
-                                                         Planes16 pl, int row0 = 0, int zrow = 0) {
+                                                         Planes16 pl, int rhs_as = -1,
+                                                         bool inv_skip = false, int row0 = 0,
+                                                         int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
         GemmSmem32 g;
@@ -428,6 +430,12 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
         }
         b = (int)(lin % nchains);
         i = K + (int)(lin / nchains);
+        // explicit-inverse panels (k_panel_inv_gemm32): this launch walks the diagonal block and
+        // the right-hand-side row only, the last logical row being that row
+        if (rhs_as >= 0 && i == Kend) i = rhs_as;
+        // ... or the whole panel, the rows below the diagonal block of the fp16x3 chains excepted
+        // (a batch with a chain outside fp16's range: those chains walk, the others do not)
+        if (inv_skip && i >= Kend && i < hlim && (!h3ok || h3ok[b])) return;
     }
     const bool pub = !BULK && i < Kend;  // rows of the diagonal block: later rows wait on them
     unsigned long long* pr = prog + b * pstride;
@@ -649,14 +657,15 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
-                            Planes16 pl) {
+                            Planes16 pl, int rhs_as, bool inv_skip) {
     // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
     // caller raises) instead of being left unfactored
     if (ncols > 14) return -1;
     if (ncols < 1 || R - K <= 1) return 0;  // (one column: its panel TRSM)
     const long grid = (long)(R - K) * nchains;
     hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
-                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc, pl);
+                       ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc, pl,
+                       rhs_as, inv_skip);
     return grid;
 }
 
@@ -667,7 +676,7 @@ void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zro
     hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
                        (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0},
-                       Planes16{nullptr, 0, 0, 0}, row0, zrow);
+                       Planes16{nullptr, 0, 0, 0}, -1, false, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -1215,6 +1224,258 @@ void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, in
     if (nq <= 0 || !pl.base) return;
     hipLaunchKernelGGL(k_chol_update32_q256, dim3((unsigned)((long)nq * nchains)), dim3(512), 0, s,
                        A, k0, kc, quads, nq, nchains, live, h3ok, pl);
+}
+
+// ------------------------------------------------------------------------- explicit-inverse panel
+// The rows below an outer panel's 512x512 diagonal block L_D solve X_i L_D^T = A_i. The dataflow
+// walk does that per row tile as 8 dependent column steps (left-looking update, TRSM by the
+// 64x64 inverse), each re-reading the row's earlier panel tiles (~95 us per walk, ~120 TFLOP/s
+// fp32-equivalent). Here the diagonal block's inverse Z = inv(L_D) (lower triangular) is formed
+// once per chain and panel, and every row tile becomes one GEMM X_i = A_i Z^T with independent
+// output columns: X_i[:, c] = sum_{k <= c} A_i[:, k] Z_ck^T. Rounding differs from the walk's
+// (the fp64 refinement, not bitwise equality, pins it: DESIGN.md §3.1).
+//
+// k_panel_zt32: workgroup (chain b, block column j) forms column j of Z by block forward
+// substitution, Z_jj = inv(L_jj), Z_ij = -inv(L_ii) sum_{k=j}^{i-1} L_ik Z_kj, in fp32 MFMA and in
+// transposed form (ZT_ji = -(ZT_j[:, j..i-1] L_i[:, j..i-1]^T) inv(L_ii)^T, the nt shape of
+// tile_gemm_nt32 and of the dataflow kernel's TRSM), keeping ZT in fp32 scratch (its own later
+// steps read it) and writing Z as fp16x3 planes (512 rows) for the GEMM.
+__device__ __forceinline__ void zput16(unsigned short* Z, const Planes16& zp, int zr, int zc,
+                                       float v) {
+    const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
+    const int64_t o = ((int64_t)(zc >> 5) * zp.rows + zr) * 32 + (zc & 31);
+    Z[o] = __builtin_bit_cast(unsigned short, h);
+    Z[o + zp.lo] = __builtin_bit_cast(unsigned short, l);
+}
+__global__ __launch_bounds__(256) void k_panel_zt32(MatF A, int K, const float* __restrict__ Dinv,
+                                                    int64_t dstride, float* zt, int64_t zstride,
+                                                    Planes16 zpl, Live live,
+                                                    const int* __restrict__ h3ok) {
+    const int b = blockIdx.x >> 3, j = blockIdx.x & 7;
+    if (!live32(live, b) || (h3ok && !h3ok[b])) return;
+    __shared__ GemmSmem32 sm;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    float* ZT = zt + b * zstride;  // ZT[c][k] = Z[k][c], 512 x 512 row-major
+    unsigned short* Zp = zpl.base + b * zpl.cstride;
+    const float* Ab = A.base + b * A.cstride;
+    {  // Z_jj = inv(L_jj) (row-major in Dinv)
+        const float* D = Dinv + b * dstride + (int64_t)(K + j) * 4096;
+        for (int e = tid; e < 4096; e += 256) {
+            const int r = e >> 6, c = e & 63;
+            const float v = D[e];
+            ZT[(int64_t)(64 * j + c) * 512 + 64 * j + r] = v;
+            zput16(Zp, zpl, 64 * j + r, 64 * j + c, v);
+        }
+    }
+    for (int i = j + 1; i < 8; ++i) {
+        // this workgroup's ZT stores drained and the CU's L1 refreshed before they are re-read
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        f4_t acc[2][2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+        // S^T = ZT_j[:, j..i-1] L_i[:, j..i-1]^T
+        tile_gemm_nt32<false>(acc, ZT + (int64_t)(64 * j) * 512 + 64 * j, 512,
+                              Ab + (int64_t)((K + i) * 64) * A.ld + (K + j) * 64, A.ld,
+                              64 * (i - j), sm, nullptr, 0);
+        // ZT_ji = -S^T inv(L_ii)^T (staged as the dataflow kernel's TRSM: A operand S^T, B
+        // operand inv(L_ii) row-major)
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sm.a[wc][32 * wr + 16 * bi + F32_CROW(lane, r)][16 * bj + r16] = acc[bi][bj][r];
+        {
+            const float* D = Dinv + b * dstride + (int64_t)(K + i) * 4096;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const int p = tid + 256 * h, row = p >> 4, col = 4 * (p & 15);
+                const f4_t v = *reinterpret_cast<const f4_t*>(D + row * 64 + col);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sm.b[col >> 5][row][(col & 31) + e] = v[e];
+            }
+        }
+        __syncthreads();
+        f4_t x[2][2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) x[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cur = 0; cur < 2; ++cur)
+#pragma unroll
+            for (int t = 0; t < KS32 / 4; ++t) {
+                float a[2], bb[2];
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi) a[bi] = sm.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj) bb[bj] = sm.b[cur][32 * wc + 16 * bj + r16][4 * t + kq];
+#pragma unroll
+                for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                    for (int bj = 0; bj < 2; ++bj)
+                        x[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj], x[bi][bj],
+                                                                        0, 0, 0);
+            }
+        // x[r][c] = ZT_ji[r][c] = Z[64i + c][64j + r]
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
+                    const float v = -x[bi][bj][r];
+                    ZT[(int64_t)(64 * j + rr) * 512 + 64 * i + cc] = v;
+                    zput16(Zp, zpl, 64 * i + cc, 64 * j + rr, v);
+                }
+        __syncthreads();  // (sm is restaged by the next step's GEMM)
+    }
+}
+
+// k_panel_inv_gemm32: workgroup (chain b, row tile i in [Kend, nb)) computes X_i = A_i Z^T for
+// the panel's 8 column tiles in fp16x3 (A_i split while staged, Z from its planes by LDS-DMA);
+// wave w owns column tiles w and 7 - w (depths w + 1 and 8 - w tiles: 9 each), so the workgroup
+// reads its row tile whole before it writes X_i in place (and the panel's planes for the
+// trailing update). 144 KB of LDS: one workgroup per CU.
+struct __attribute__((aligned(16))) InvGemmSmem {
+    _Float16 a[2][2][64][LPH];   // [buffer][hi, lo][row][k] (HS layout)
+    _Float16 z[2][2][512][LPH];  // [buffer][hi, lo][Z row][k]
+};
+__global__ __launch_bounds__(256, 1) void k_panel_inv_gemm32(MatF A, int K, int Kend, int nb,
+                                                             Planes16 zpl, Planes16 pl, Live live,
+                                                             int nchains,
+                                                             const int* __restrict__ h3ok) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r16 = lane & 15, kq = lane >> 4;
+    __shared__ InvGemmSmem sm;
+    const int nrows = nb - Kend;
+    const long w = xcd_remap32((long)blockIdx.x, (long)nrows * nchains);
+    const int b = (int)(w / nrows), i = Kend + (int)(w % nrows);
+    if (!live32(live, b) || (h3ok && !h3ok[b])) return;
+    float* Ai = A.base + b * A.cstride + (int64_t)(i * 64) * A.ld + K * 64;
+    const int c0 = wv, c1 = 7 - wv;
+    f4_t acc0[4][4], acc1[4][4];
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj) {
+            acc0[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+            acc1[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+        }
+    // A staging: thread t moves row t/4, k 8(t%4) .. +7 of the 32-deep slice (split in registers)
+    const int arow = tid >> 2, acol = 8 * (tid & 3);
+    const float* ag = Ai + (int64_t)arow * A.ld + acol;
+    f4_t ra0, ra1;
+    auto aload = [&](int sidx) {
+        ra0 = *reinterpret_cast<const f4_t*>(ag + KS128 * sidx);
+        ra1 = *reinterpret_cast<const f4_t*>(ag + KS128 * sidx + 4);
+    };
+    auto astore = [&](int buf) {
+        h4_t h0, l0, h1, l1;
+        split_h3(ra0, h0, l0);
+        split_h3(ra1, h1, l1);
+        const h8_t hi = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const h8_t lo = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        *reinterpret_cast<h8_t*>(&sm.a[buf][0][arow][HS(arow, acol)]) = hi;
+        *reinterpret_cast<h8_t*>(&sm.a[buf][1][arow][HS(arow, acol)]) = lo;
+    };
+    // Z staging by LDS-DMA: rows [64 kb, 512) of slice s (the column tiles that need it); wave
+    // wv takes plane wv & 1 and the 16-row groups g = (wv >> 1) + 2t; lane l: row 16g + l/4,
+    // LDS slot l%4 = logical piece (l%4) ^ (bit 3 of the row)
+    const int rowl = lane >> 2, piece = (lane & 3) ^ ((rowl >> 2) & 2), pln = wv & 1;
+    const unsigned short* zg = zpl.base + b * zpl.cstride + (pln ? zpl.lo : 0) +
+                               (int64_t)rowl * 32 + piece * 8;
+    auto dma = [&](int sidx, int buf) {
+        const int kb = sidx >> 1;
+        for (int g = 4 * kb + (wv >> 1); g < 32; g += 2)
+            __builtin_amdgcn_global_load_lds(
+                (glb_void_t*)(zg + ((int64_t)sidx * zpl.rows + 16 * g) * 32),
+                (lds_void_t*)&sm.z[buf][pln][16 * g][0], 16, 0, 0);
+    };
+    auto mm = [&](f4_t (&acc)[4][4], int cc, int cur) {
+        h8_t bh[4], bl[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const int row = 64 * cc + 16 * x + r16;
+            bh[x] = *reinterpret_cast<const h8_t*>(&sm.z[cur][0][row][HS(row, 8 * kq)]);
+            bl[x] = *reinterpret_cast<const h8_t*>(&sm.z[cur][1][row][HS(row, 8 * kq)]);
+        }
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi) {
+            const int row = 16 * bi + r16;
+            const h8_t ah = *reinterpret_cast<const h8_t*>(&sm.a[cur][0][row][HS(row, 8 * kq)]);
+            const h8_t al = *reinterpret_cast<const h8_t*>(&sm.a[cur][1][row][HS(row, 8 * kq)]);
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj) {
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[bj], acc[bi][bj], 0, 0, 0);
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[bj], acc[bi][bj], 0, 0, 0);
+                acc[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[bj], acc[bi][bj], 0, 0, 0);
+            }
+        }
+    };
+    constexpr int nsub = 512 / KS128;
+    aload(0);
+    dma(0, 0);
+    astore(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nsub; ++s) {
+        if (s + 1 < nsub) {
+            aload(s + 1);
+            dma(s + 1, (s + 1) & 1);
+        }
+        const int kb = s >> 1;
+        if (kb <= c0) mm(acc0, c0, s & 1);
+        if (kb <= c1) mm(acc1, c1, s & 1);
+        if (s + 1 < nsub) astore((s + 1) & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // X_i in place (the whole row tile was read above) and the panel's planes
+    const bool planes = pl.base && (i + 1) * 64 <= pl.rows;
+    auto put = [&](const f4_t (&acc)[4][4], int cc) {
+        unsigned short* hp = planes ? pl.base + b * pl.cstride : nullptr;
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = 16 * bi + F32_CROW(lane, r), col = 64 * cc + 16 * bj + r16;
+                    const float v = acc[bi][bj][r];
+                    Ai[(int64_t)rr * A.ld + col] = v;
+                    if (planes) {
+                        const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
+                        const int64_t o =
+                            ((int64_t)(col >> 5) * pl.rows + i * 64 + rr) * 32 + (col & 31);
+                        hp[o] = __builtin_bit_cast(unsigned short, h);
+                        hp[o + pl.lo] = __builtin_bit_cast(unsigned short, l);
+                    }
+                }
+    };
+    put(acc0, c0);
+    put(acc1, c1);
+}
+
+void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
+                        int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
+                        const int* h3ok, hipStream_t s) {
+    hipLaunchKernelGGL(k_panel_zt32, dim3((unsigned)(8 * nchains)), dim3(256), 0, s, A, K, Dinv,
+                       dstride, zt, zstride, zpl, live, h3ok);
+    const int Kend = K + 8;
+    if (nb > Kend)
+        hipLaunchKernelGGL(k_panel_inv_gemm32, dim3((unsigned)((long)(nb - Kend) * nchains)),
+                           dim3(256), 0, s, A, K, Kend, nb, zpl, pl, live, nchains, h3ok);
 }
 
 // Host: 256x256 quad tiles covering tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in

@@ -383,10 +383,10 @@ def test_update_operand_planes_bitwise(nat, monkeypatch, n):
     batch (fp32 operands) the quad path falls back to the 128-row kernel for the whole call,
     again bitwise."""
     X, y, thetas, ns = _mixed_case(n=n)
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_PLANES=0)
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_PLANES=0, APM_DFINV=0)
     assert (s0 == 0).all()
     for env in ({}, {'APM_Q256': 0}):
-        o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, **env)
+        o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0, **env)
         np.testing.assert_array_equal(s1, s0)
         np.testing.assert_array_equal(n1, n0)
         np.testing.assert_array_equal(o1, o0)
@@ -394,14 +394,47 @@ def test_update_operand_planes_bitwise(nat, monkeypatch, n):
             np.testing.assert_array_equal(f1[b], f0[b])
     big = thetas.copy()
     big[2, 0] = 19.5
-    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_PLANES=0)
-    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch)
+    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_PLANES=0, APM_DFINV=0)
+    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch, APM_DFINV=0)
     np.testing.assert_array_equal(sb1, sb0)
     np.testing.assert_array_equal(nb1, nb0)
     np.testing.assert_array_equal(ob1, ob0)
     for b in range(len(big)):
         if sb0[b] == 0:  # (a failed chain's slot is not written)
             np.testing.assert_array_equal(fb1[b], fb0[b])
+
+
+@pytest.mark.parametrize('n', [2048, 700])
+def test_explicit_inverse_panels_match_walk(nat, monkeypatch, n):
+    """The explicit-inverse panels of the Newton factorisation (default; chol32.hip
+    k_panel_zt32 + k_panel_inv_gemm32: Z = inv(L_D) of each 512x512 diagonal block, then one
+    fp16x3 GEMM X_i = A_i Z^T per row tile below it) against the dataflow walk (APM_DFINV=0):
+    the rounding of the factor differs (the product with inv(L_D) amplifies its 22-bit fp16x3
+    operands by cond(L_D), where the walk's TRSM by the 64x64 inverses is fp32), the fp64
+    refinement makes the Newton modes agree to 1e-8 of their maximum (the f_post tolerance of
+    DESIGN.md §3.3; ~5e-9 measured at n = 2048) and the estimates to 1e-6, with the same
+    iteration counts. n = 700: one
+    full panel and a ragged last one (walked). A chain outside fp16's range walks its panels
+    (bitwise the walk) while the other chains of its batch keep the inverse panels (bitwise
+    their values without it): a chain's value does not depend on its batch."""
+    X, y, thetas, ns = _mixed_case(n=n)
+    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    assert (s0 == 0).all() and (s1 == 0).all()
+    np.testing.assert_array_equal(n1, n0)
+    for b in range(len(thetas)):
+        np.testing.assert_allclose(f1[b], f0[b], rtol=0, atol=1e-8 * np.abs(f0[b]).max())
+        assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
+    big = thetas.copy()
+    big[2, 0] = 19.5
+    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_DFINV=0)
+    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch)
+    np.testing.assert_array_equal(sb1, sb0)
+    np.testing.assert_array_equal(nb1, nb0)
+    assert ob1[2] == ob0[2] or (sb0[2] != 0)
+    for b in (0, 1):
+        np.testing.assert_array_equal(fb1[b], f1[b])
+        assert ob1[b] == o1[b]
 
 
 def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
@@ -465,15 +498,16 @@ def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch, n):
     for a batch with a chain at an extreme theta (fp32 operands, possibly a failed fp32
     factorisation and its fp64 rerun) next to ordinary ones: the per-column launch sequence
     (APM_DF32=0) and the default, one dataflow launch per outer panel whose rows walk the panel's
-    columns (k_chol_panel_df32). n = 560: a last outer panel of one column (its TRSM only),
-    n = 1100: three outer panels, the last of two."""
+    columns (k_chol_panel_df32; the explicit-inverse panels off, APM_DFINV=0: they round
+    differently, test_explicit_inverse_panels_match_walk). n = 560: a last outer panel of one
+    column (its TRSM only), n = 1100: three outer panels, the last of two."""
     X, y, thetas, ns = _mixed_case(n=n)
     ext = thetas[0].copy()
     ext[0] = 45.0
     thetas = np.vstack([thetas, ext])
     o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0)
     assert (s0[:3] == 0).all()
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
+    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0)
     np.testing.assert_array_equal(s1, s0)
     np.testing.assert_array_equal(n1, n0)
     for b in range(len(thetas)):
