@@ -114,8 +114,8 @@ long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
                             bool inv_skip = false);
 // explicit-inverse panel of the Newton factorisation (chol32.hip), after a dataflow launch over
 // the diagonal block [K, K+8) and the right-hand-side row (rhs_as): Z = inv(L_D) of the 512x512
-// diagonal block as fp16x3 planes (zpl, 512 rows), with ZT = Z^T in fp32 scratch (zt: 512 x 512
-// per chain, zstride floats apart); then every row tile i in [K+8, nb) of the panel becomes
+// diagonal block as fp16x3 planes (zpl, 512 rows), by recursive doubling over fp32 scratch (zt:
+// 3 x 512 x 512 per chain, zstride floats apart); then every row tile i in [K+8, nb) becomes
 // X_i = A_i Z^T in one fp16x3 GEMM (in place, plus the panel's planes pl). Chains with h3ok only.
 void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
                         int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
@@ -140,7 +140,8 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
                                Live live, int nchains, hipStream_t s,
                                FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
                                int hlim = 0, const int* h3ok = nullptr, int rhs = -1,
-                               int role = 0,  // role 1: the posterior bottom block (a name only)
+                               int role = 0,  // 1: the posterior bottom block, 3: the rhs row
+                                              // alone (names only)
                                Planes16 pl = Planes16{nullptr, 0, 0, 0});  // k0's panel's planes
 // the far trailing updates of the Newton factorisation on 256x256 quad tiles (chol32.hip): fp16x3
 // operands from the planes only, rows below the appended right-hand side, chains with h3ok set

@@ -120,9 +120,9 @@ struct apm_ctx {
     bool planes_on = true;
     unsigned short* planes = nullptr;
     int64_t plane_cs = 0;  // halves per chain and buffer
-    // explicit-inverse panels (APM_DFINV, chol32.hip k_panel_zt32 / k_panel_inv_gemm32): the
+    // explicit-inverse panels (APM_DFINV, chol32.hip k_zinv_* / k_panel_inv_gemm32): the
     // dataflow launch walks the diagonal block and the right-hand-side row only; Z = inv(L_D) per
-    // chain (fp32 transposed scratch zt, fp16x3 planes zplanes) and one GEMM per row tile below
+    // chain (fp32 scratch zt: Z, Z^T, T^T; fp16x3 planes zplanes) and one GEMM per row tile below
     bool dfinv = true;
     float* zt = nullptr;
     unsigned short* zplanes = nullptr;
@@ -449,34 +449,37 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     FusedDiag<float> fd{0, nullptr, 0, nullptr, 0, 0};
     if (fuse_k >= 0)
         fd = FusedDiag<float>{1, dinv32_of(c), 2 * c->dstride, c->ldet, c->lstride, fail_code};
-    const double fl = c->prof ? update_flops(i0, R, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
-    ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl, st);
-    ProfScope ps_outer(c, kc >= 2 && jend - j0 >= 2 ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl, st);
-    if (kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k))) {
-        // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a
-        // row vector (rhs_row_update32)
-        const int rhs = R > c->nb ? c->nb : -1;
-        if (pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb) {
-            // rows above the right-hand side on quad tiles, that row on the 128-row kernel
-            const auto ql = quad_list(c, i0, std::min(R, c->nb), j0, jend);
+    const bool outer = kc >= 2 && jend - j0 >= 2 && (fuse_k < 0 || (i0 == fuse_k && j0 == fuse_k));
+    // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a row
+    // vector (rhs_row_update32); with the quad tiles that row is a launch of its own (role 3,
+    // outside the profiled scope: the roofline's launches are the quad and 128-row GEMMs)
+    const int rhs = R > c->nb ? c->nb : -1;
+    const bool quad = outer && pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb;
+    {
+        const int Rg = quad ? std::min(R, c->nb) : R;
+        const double fl = c->prof ? update_flops(i0, Rg, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
+        ProfScope ps(c, APM_PROF_CHOL_UPDATE32, fl, st);
+        ProfScope ps_outer(c, outer ? APM_PROF_CHOL_UPDATE32_OUTER : -1, fl, st);
+        if (quad) {
+            const auto ql = quad_list(c, i0, Rg, j0, jend);
             launch_chol_update32_q256(M, k0, kc, ql.first, ql.second, live_of(c), count, st,
                                       c->h3ok, pl);
-            if (rhs >= 0) {
-                check_launch();
-                const auto sl = super_list(c, c->nb, R, j0, jend, Gap{0, 0}, rhs);
-                launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st,
-                                          fd, c->nb, c->h3ok, rhs, 0, pl);
-            }
-        } else {
+        } else if (outer) {
             const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
             launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
                                       c->h3_now ? c->nb : 0, c->h3ok, rhs, 0, pl);
+        } else {
+            launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, st, fd,
+                                 c->h3_now ? c->nb : 0, c->h3ok);
         }
-    } else {
-        launch_chol_update32(M, k0, kc, tl.first, tl.second, live_of(c), count, st, fd,
-                             c->h3_now ? c->nb : 0, c->h3ok);
+        check_launch();
     }
-    check_launch();
+    if (quad && rhs >= 0) {
+        const auto sl = super_list(c, c->nb, R, j0, jend, Gap{0, 0}, rhs);
+        launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
+                                  c->nb, c->h3ok, rhs, 3, pl);
+        check_launch();
+    }
 }
 
 // chol_range's twin for the fp32 Newton matrix (same steps, same fused diag)
@@ -513,7 +516,7 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
             c->ticket_base += (unsigned long long)tickets;
             if (inv) {  // the rows below the diagonal block: X_i = A_i inv(L_D)^T
                 const int64_t zcs = 2 * 16 * 512 * 32;
-                launch_panel_inv32(M, K, c->nb, D, ds, c->zt, 512 * 512,
+                launch_panel_inv32(M, K, c->nb, D, ds, c->zt, 3 * 512 * 512,
                                    Planes16{c->zplanes, zcs, zcs / 2, 512}, planes_of(c, K), lv,
                                    count, c->h3ok, c->stream);
                 check_launch();
@@ -1303,7 +1306,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
         c->plane_cs = 2 * np * 32 * 2 * c->outer32;  // 2 planes x rows x 2 outer32 slices x 32
         c->planes = dalloc<unsigned short>(c, 2 * B * c->plane_cs);
         if (c->dfinv && c->outer32 == 8) {
-            c->zt = dalloc<float>(c, B * 512 * 512);
+            c->zt = dalloc<float>(c, B * 3 * 512 * 512);
             c->zplanes = dalloc<unsigned short>(c, B * 2 * 16 * 512 * 32);
         }
     }

@@ -769,7 +769,8 @@ __device__ __forceinline__ void rhs_row_update32(float* Ab, int64_t ld, int ti, 
 // ROLE 0: the Newton factorisation, 1: the posterior factor's bottom block (postcov.hip; the same
 // code, a separate instantiation so that the two launch populations get separate rocprofv3
 // counter figures), 2: the Newton factorisation with the fp16x3 operands read from the dataflow
-// kernel's planes (Planes16) instead of split while staged
+// kernel's planes (Planes16) instead of split while staged, 3: the right-hand-side row tile alone
+// beside the quad-tile kernel (a name only)
 template <bool H3, int ROLE>
 __global__ __launch_bounds__(256, 2) void k_chol_update32_t128(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ tiles,
@@ -1086,7 +1087,8 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
                        k0, kc, tiles, ntiles, nchains, live, fd, H ? hlim : 0,               \
                        H ? h3ok : nullptr, rhs, pl)
     if (hlim > 0) {
-        if (pl.base) UPD32_LAUNCH(true, 2);
+        if (role == 3) UPD32_LAUNCH(true, 3);  // the right-hand-side row alone
+        else if (pl.base) UPD32_LAUNCH(true, 2);
         else if (role) UPD32_LAUNCH(true, 1);
         else UPD32_LAUNCH(true, 0);
     } else {
@@ -1235,11 +1237,13 @@ void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, in
 // output columns: X_i[:, c] = sum_{k <= c} A_i[:, k] Z_ck^T. Rounding differs from the walk's
 // (the fp64 refinement, not bitwise equality, pins it: DESIGN.md §3.1).
 //
-// k_panel_zt32: workgroup (chain b, block column j) forms column j of Z by block forward
-// substitution, Z_jj = inv(L_jj), Z_ij = -inv(L_ii) sum_{k=j}^{i-1} L_ik Z_kj, in fp32 MFMA and in
-// transposed form (ZT_ji = -(ZT_j[:, j..i-1] L_i[:, j..i-1]^T) inv(L_ii)^T, the nt shape of
-// tile_gemm_nt32 and of the dataflow kernel's TRSM), keeping ZT in fp32 scratch (its own later
-// steps read it) and writing Z as fp16x3 planes (512 rows) for the GEMM.
+// Z = inv(L_D) by recursive doubling in 64-tile units (fp32 MFMA): with L_D split into
+// [[L11, 0], [L21, L22]] of m x m tiles, Z21 = -Z22 (L21 Z11). Level m = 1, 2, 4 takes the
+// 8 / (2m) diagonal pairs of the level at once, each in two batched tile-product launches
+// (T = L21 Z11, then Z21 = -Z22 T), so Z needs 1 + 3 x 2 dependent launches of 64x64 tile
+// products (depth <= 4 tiles) instead of a 7-step substitution per column (150-270 us per panel
+// at 64 chains, round 5). Scratch per chain (zt, 3 x 512 x 512 fp32): Z row-major, Z^T, and T^T,
+// the operands of tile_gemm_nt32's A B^T form; Z also goes out as fp16x3 planes (512 rows).
 __device__ __forceinline__ void zput16(unsigned short* Z, const Planes16& zp, int zr, int zc,
                                        float v) {
     const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
@@ -1247,100 +1251,76 @@ __device__ __forceinline__ void zput16(unsigned short* Z, const Planes16& zp, in
     Z[o] = __builtin_bit_cast(unsigned short, h);
     Z[o + zp.lo] = __builtin_bit_cast(unsigned short, l);
 }
-__global__ __launch_bounds__(256) void k_panel_zt32(MatF A, int K, const float* __restrict__ Dinv,
-                                                    int64_t dstride, float* zt, int64_t zstride,
-                                                    Planes16 zpl, Live live,
-                                                    const int* __restrict__ h3ok) {
-    const int b = blockIdx.x >> 3, j = blockIdx.x & 7;
+#define ZS 512  // scratch leading dimension
+// diagonal tiles: Z_ii = inv(L_ii) (row-major in Dinv)
+__global__ __launch_bounds__(256) void k_zinv_diag32(int K, const float* __restrict__ Dinv,
+                                                     int64_t dstride, float* zt, int64_t zstride,
+                                                     Planes16 zpl, Live live,
+                                                     const int* __restrict__ h3ok) {
+    const int b = blockIdx.x >> 3, i = blockIdx.x & 7;
     if (!live32(live, b) || (h3ok && !h3ok[b])) return;
+    float* Zr = zt + b * zstride;
+    float* ZT = Zr + ZS * ZS;
+    unsigned short* Zp = zpl.base + b * zpl.cstride;
+    const float* D = Dinv + b * dstride + (int64_t)(K + i) * 4096;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        const float v = D[e];
+        Zr[(int64_t)(64 * i + r) * ZS + 64 * i + c] = v;
+        ZT[(int64_t)(64 * i + c) * ZS + 64 * i + r] = v;
+        zput16(Zp, zpl, 64 * i + r, 64 * i + c, v);
+    }
+}
+// one stage of level m: workgroup (chain, pair p, output tile (a, b)) of the pair whose L21 sits at
+// tile rows r0 = 2mp + m, columns c0 = 2mp. mode 0: T_ab = sum_{k=b}^{m-1} L21_ak Z11_kb, stored
+// transposed; mode 1: Z21_ab = -sum_{k=0}^{a} Z22_ak T_kb, stored as Z, Z^T and planes
+__global__ __launch_bounds__(256) void k_zinv_step32(MatF A, int K, int m, int mode, float* zt,
+                                                     int64_t zstride, Planes16 zpl, Live live,
+                                                     const int* __restrict__ h3ok) {
+    const int per = 4 / m * m * m;  // output tiles per chain: (8 / 2m) pairs x m x m
+    const int b = blockIdx.x / per, w = blockIdx.x % per;
+    if (!live32(live, b) || (h3ok && !h3ok[b])) return;
+    const int p = w / (m * m), ta = (w % (m * m)) / m, tb = w % m;
+    const int r0 = 2 * m * p + m, c0 = 2 * m * p;
     __shared__ GemmSmem32 sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
-    const int r16 = lane & 15, kq = lane >> 4;
-    float* ZT = zt + b * zstride;  // ZT[c][k] = Z[k][c], 512 x 512 row-major
+    const int r16 = lane & 15;
+    float* Zr = zt + b * zstride;
+    float* ZT = Zr + ZS * ZS;
+    float* Tt = ZT + ZS * ZS;
+    f4_t acc[2][2];
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+    if (mode == 0) {
+        const float* L = A.base + b * A.cstride + (int64_t)((K + r0 + ta) * 64) * A.ld +
+                         (K + c0 + tb) * 64;
+        tile_gemm_nt32<false>(acc, L, A.ld, ZT + (int64_t)((c0 + tb) * 64) * ZS + (c0 + tb) * 64,
+                              ZS, 64 * (m - tb), sm, nullptr, 0);
+    } else {
+        tile_gemm_nt32<true>(acc, Zr + (int64_t)((r0 + ta) * 64) * ZS + r0 * 64, ZS,
+                             Tt + (int64_t)((c0 + tb) * 64) * ZS + r0 * 64, ZS, 64 * (ta + 1),
+                             sm, nullptr, 0);
+    }
     unsigned short* Zp = zpl.base + b * zpl.cstride;
-    const float* Ab = A.base + b * A.cstride;
-    {  // Z_jj = inv(L_jj) (row-major in Dinv)
-        const float* D = Dinv + b * dstride + (int64_t)(K + j) * 4096;
-        for (int e = tid; e < 4096; e += 256) {
-            const int r = e >> 6, c = e & 63;
-            const float v = D[e];
-            ZT[(int64_t)(64 * j + c) * 512 + 64 * j + r] = v;
-            zput16(Zp, zpl, 64 * j + r, 64 * j + c, v);
-        }
-    }
-    for (int i = j + 1; i < 8; ++i) {
-        // this workgroup's ZT stores drained and the CU's L1 refreshed before they are re-read
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        f4_t acc[2][2];
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-        // S^T = ZT_j[:, j..i-1] L_i[:, j..i-1]^T
-        tile_gemm_nt32<false>(acc, ZT + (int64_t)(64 * j) * 512 + 64 * j, 512,
-                              Ab + (int64_t)((K + i) * 64) * A.ld + (K + j) * 64, A.ld,
-                              64 * (i - j), sm, nullptr, 0);
-        // ZT_ji = -S^T inv(L_ii)^T (staged as the dataflow kernel's TRSM: A operand S^T, B
-        // operand inv(L_ii) row-major)
+        for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    sm.a[wc][32 * wr + 16 * bi + F32_CROW(lane, r)][16 * bj + r16] = acc[bi][bj][r];
-        {
-            const float* D = Dinv + b * dstride + (int64_t)(K + i) * 4096;
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const int p = tid + 256 * h, row = p >> 4, col = 4 * (p & 15);
-                const f4_t v = *reinterpret_cast<const f4_t*>(D + row * 64 + col);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) sm.b[col >> 5][row][(col & 31) + e] = v[e];
-            }
-        }
-        __syncthreads();
-        f4_t x[2][2];
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj) x[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int cur = 0; cur < 2; ++cur)
-#pragma unroll
-            for (int t = 0; t < KS32 / 4; ++t) {
-                float a[2], bb[2];
-#pragma unroll
-                for (int bi = 0; bi < 2; ++bi) a[bi] = sm.a[cur][32 * wr + 16 * bi + r16][4 * t + kq];
-#pragma unroll
-                for (int bj = 0; bj < 2; ++bj) bb[bj] = sm.b[cur][32 * wc + 16 * bj + r16][4 * t + kq];
-#pragma unroll
-                for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-                    for (int bj = 0; bj < 2; ++bj)
-                        x[bi][bj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[bi], bb[bj], x[bi][bj],
-                                                                        0, 0, 0);
-            }
-        // x[r][c] = ZT_ji[r][c] = Z[64i + c][64j + r]
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
-                    const float v = -x[bi][bj][r];
-                    ZT[(int64_t)(64 * j + rr) * 512 + 64 * i + cc] = v;
-                    zput16(Zp, zpl, 64 * i + cc, 64 * j + rr, v);
+            for (int r = 0; r < 4; ++r) {
+                const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
+                const float v = acc[bi][bj][r];
+                const int zr = (r0 + ta) * 64 + rr, zc = (c0 + tb) * 64 + cc;
+                if (mode == 0) {
+                    Tt[(int64_t)zc * ZS + zr] = v;
+                } else {
+                    Zr[(int64_t)zr * ZS + zc] = v;
+                    ZT[(int64_t)zc * ZS + zr] = v;
+                    zput16(Zp, zpl, zr, zc, v);
                 }
-        __syncthreads();  // (sm is restaged by the next step's GEMM)
-    }
+            }
 }
 
 // k_panel_inv_gemm32: workgroup (chain b, row tile i in [Kend, nb)) computes X_i = A_i Z^T for
@@ -1470,8 +1450,12 @@ __global__ __launch_bounds__(256, 1) void k_panel_inv_gemm32(MatF A, int K, int 
 void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
                         int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
                         const int* h3ok, hipStream_t s) {
-    hipLaunchKernelGGL(k_panel_zt32, dim3((unsigned)(8 * nchains)), dim3(256), 0, s, A, K, Dinv,
+    hipLaunchKernelGGL(k_zinv_diag32, dim3((unsigned)(8 * nchains)), dim3(256), 0, s, K, Dinv,
                        dstride, zt, zstride, zpl, live, h3ok);
+    for (int m = 1; m <= 4; m *= 2)
+        for (int mode = 0; mode < 2; ++mode)
+            hipLaunchKernelGGL(k_zinv_step32, dim3((unsigned)(4 * m * nchains)), dim3(256), 0, s,
+                               A, K, m, mode, zt, zstride, zpl, live, h3ok);
     const int Kend = K + 8;
     if (nb > Kend)
         hipLaunchKernelGGL(k_panel_inv_gemm32, dim3((unsigned)((long)(nb - Kend) * nchains)),

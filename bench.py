@@ -848,12 +848,15 @@ def main():
                           'of the fp64 factorisations: chol(K), the single-launch SYRK and the '
                           'chol of I + L_K^T W L_K)', PEAK_F64_MFMA_TFLOPS,
                           ('k_chol_update_t128',), 'f64')
-    upd32 = mfma_roofline('chol_update32', 'k_chol_update32_t128 (rank-512 trailing updates of '
-                          'the Newton factorisation of B, fp16x3: fp32 operands split into fp16 '
-                          'hi/lo, 3 v_mfma_f32_16x16x32_f16 per block, fp32 accumulation; '
+    upd32 = mfma_roofline('chol_update32', 'k_chol_update32_q256 + k_chol_update32_t128 '
+                          '(rank-512 trailing updates of the Newton factorisation of B, fp16x3: '
+                          'operands as fp16 hi/lo planes written by the panel kernels, 3 '
+                          'v_mfma_f32_16x16x32_f16 per block, fp32 accumulation; the far part on '
+                          '256x256 quad tiles, the next panel\'s columns on 128x128 super-tiles; '
                           'achieved in fp32-equivalent flops against the fp16 peak / 3)',
                           PEAK_F16X3_TFLOPS,
-                          ('k_chol_update32_t128<true, 0>', 'k_chol_update32_t128<false, 0>'),
+                          ('k_chol_update32_q256', 'k_chol_update32_t128<true, 2>',
+                           'k_chol_update32_t128<true, 0>', 'k_chol_update32_t128<false, 0>'),
                           'f16x3')
     # the posterior factor's fp32 bottom block: the same kernel under its own instantiation name
     # (ROLE = 1, chol32.hip), so its counter figures are its own

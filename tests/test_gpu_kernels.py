@@ -332,21 +332,26 @@ def _run_is(nat, X, y, thetas, ns, monkeypatch, **env):
 
 
 def test_mixed_newton_matches_fp64(nat, monkeypatch):
-    """The fp32 factorisation of B + one fp64 refinement step (chol32.hip) reproduces the fp64
-    Newton mode (1e-9 relative here; 1e-12 typical) and hence the estimate, for sigma = e^0..e^4."""
+    """The fp32 factorisation of B + fp64 refinement (chol32.hip) reproduces the fp64 Newton mode
+    within the f_post tolerance, 1e-8 of its maximum (~1e-12 with the dataflow
+    walk, ~1e-9 with the explicit-inverse panels, whose fp16x3 product with inv(L_D) leaves a
+    less accurate factor for the refinement to correct), and hence the estimate, for
+    sigma = e^0..e^4."""
     X, y, thetas, ns = _mixed_case()
     o64, s64, n64, f64 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=0)
     o32, s32, n32, f32 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_MIXED=1)
     assert (s64 == 0).all() and (s32 == 0).all()
     np.testing.assert_array_equal(n32, n64)
     for b in range(len(thetas)):
-        np.testing.assert_allclose(f32[b], f64[b], rtol=1e-9, atol=1e-9 * np.abs(f64[b]).max())
+        np.testing.assert_allclose(f32[b], f64[b], rtol=0, atol=1e-8 * np.abs(f64[b]).max())
         assert abs(o32[b] - o64[b]) <= 1e-6 * max(1.0, abs(o64[b])), (b, o32[b], o64[b])
 
 
 def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
     """fp16x3 trailing updates of the Newton factor (chol32.hip, default) against fp32 operands
-    (APM_H3=0): same iteration counts, modes to 1e-9 relative, estimates to 1e-6. The range
+    (APM_H3=0, which also walks every panel: the explicit-inverse panels need the planes): same
+    iteration counts, modes within the f_post tolerance (1e-8 of the maximum), estimates to 1e-6.
+    The range
     guard is per chain: a chain at theta_0 >= 19 takes fp32 operands (bit-identical to APM_H3=0)
     while the other chains of the same call keep fp16x3 (bit-identical to a call without it), so
     a chain's value does not depend on its batch."""
@@ -356,7 +361,7 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
     assert (s0 == 0).all() and (s1 == 0).all()
     np.testing.assert_array_equal(n1, n0)
     for b in range(len(thetas)):
-        np.testing.assert_allclose(f1[b], f0[b], rtol=1e-9, atol=1e-9 * np.abs(f0[b]).max())
+        np.testing.assert_allclose(f1[b], f0[b], rtol=0, atol=1e-8 * np.abs(f0[b]).max())
         assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
     big = thetas.copy()
     big[2, 0] = 19.5
