@@ -25,6 +25,6 @@ for p in mfma insts waits fetch write; do
   c=$(find $O/$p -name '*counter_collection.csv' | head -1)
   [ -n "$c" ] && F="$F $c"
 done
-python3 tools/pmc_kernels.py --match k_chol_update32_t128 --match k_chol_panel_df32 --match k_trsv32_mw --match k_symv_part --match k_chol_update_t128 $F --json $O/summary.json > $O/summary.txt 2>&1
+python3 tools/pmc_kernels.py --match k_chol_update32_t128 --match k_chol_update32_q256 --match k_panel_inv_gemm32 --match k_zinv --match k_chol_panel_df32 --match k_trsv32_mw --match k_symv_part --match k_chol_update_t128 $F --json $O/summary.json > $O/summary.txt 2>&1
 find $O -name '*.csv' -delete
 echo done
