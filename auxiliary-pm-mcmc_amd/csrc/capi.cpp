@@ -95,6 +95,7 @@ struct apm_ctx {
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists;
     std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_solo;
     std::map<std::tuple<int, int, int, int>, std::pair<unsigned*, int>> quad_lists;
+    std::map<std::tuple<int, int, int, int, int, int>, std::pair<unsigned*, int>> super_lists_ext;
     // 128x128 super-tile kernels for the outer updates: bit 0 fp32, bit 1 fp64 (APM_T128)
     bool h3 = true;       // APM_H3=0: fp32 operands in the fp32 factorisations' outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
@@ -425,6 +426,24 @@ std::pair<unsigned*, int> super_list(apm_ctx* c, int i0, int R, int j0, int jend
     return val;
 }
 
+// the super-tiles of (i0, R, j0, jend) with row tile rhs alone, followed by that row's super-tiles
+// of the columns [jend, jext): the next panel's columns of a lookahead update and the right-hand
+// side row's far columns in one launch
+std::pair<unsigned*, int> super_list_ext(apm_ctx* c, int i0, int R, int j0, int jend, int rhs,
+                                         int jext) {
+    auto key = std::make_tuple(i0, R, j0, jend, rhs, jext);
+    auto it = c->super_lists_ext.find(key);
+    if (it != c->super_lists_ext.end()) return it->second;
+    std::vector<unsigned> v = build_update_supertiles(i0, R, j0, jend, 0, 0, rhs);
+    const std::vector<unsigned> e = build_update_supertiles(rhs, rhs + 1, jend, jext, 0, 0, rhs);
+    v.insert(v.end(), e.begin(), e.end());
+    unsigned* d = dalloc<unsigned>(c, v.size());
+    HIPC(hipMemcpy(d, v.data(), sizeof(unsigned) * v.size(), hipMemcpyHostToDevice));
+    auto val = std::make_pair(d, (int)v.size());
+    c->super_lists_ext[key] = val;
+    return val;
+}
+
 std::pair<unsigned*, int> quad_list(apm_ctx* c, int i0, int R, int j0, int jend) {
     auto key = std::make_tuple(i0, R, j0, jend);
     auto it = c->quad_lists.find(key);
@@ -440,7 +459,7 @@ std::pair<unsigned*, int> quad_list(apm_ctx* c, int i0, int R, int j0, int jend)
 
 void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0, int jend,
                       int count, int fuse_k = -1, int fail_code = 0, hipStream_t st = nullptr,
-                      Planes16 pl = Planes16{nullptr, 0, 0, 0}) {
+                      Planes16 pl = Planes16{nullptr, 0, 0, 0}, int jext = -1) {
     if (!st) st = c->stream;
     if (i0 < j0) i0 = j0;
     if (update_tile_count(i0, R, j0, jend) <= 0) return;
@@ -465,7 +484,9 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
             launch_chol_update32_q256(M, k0, kc, ql.first, ql.second, live_of(c), count, st,
                                       c->h3ok, pl);
         } else if (outer) {
-            const auto sl = super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
+            // jext > jend: also the right-hand-side row's columns [jend, jext)
+            const auto sl = rhs >= 0 && jext > jend ? super_list_ext(c, i0, R, j0, jend, rhs, jext)
+                                                    : super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
             launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
                                       c->h3_now ? c->nb : 0, c->h3ok, rhs, 0, pl);
         } else {
@@ -531,11 +552,14 @@ void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_co
                 hipEvent_t e_df = c->ev_la[c->la_i++ & 3];
                 HIPC(hipEventRecord(e_df, c->stream));
                 if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
+                // (the right-hand-side row's far columns go with the narrow update on this
+                // stream: on stream3 behind the far update they held up the next narrow update)
                 tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Knext, count,
-                                 have_diag ? Kend : -1, fail_code, nullptr, planes_of(c, K));
+                                 have_diag ? Kend : -1, fail_code, nullptr, planes_of(c, K),
+                                 R > c->nb ? Cb : -1);
                 HIPC(hipStreamWaitEvent(c->stream3, e_df, 0));
-                tracked_update32(c, M, K, Kend - K, Knext, R, Knext, Cb, count, -1, fail_code,
-                                 c->stream3, planes_of(c, K));
+                tracked_update32(c, M, K, Kend - K, Knext, std::min(R, c->nb), Knext, Cb, count,
+                                 -1, fail_code, c->stream3, planes_of(c, K));
                 e_far = c->ev_la[c->la_i++ & 3];
                 HIPC(hipEventRecord(e_far, c->stream3));
                 far_pending = true;
