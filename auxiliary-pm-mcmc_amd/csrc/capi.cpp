@@ -472,8 +472,9 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     // the Newton matrix's appended right-hand-side row tile (nb, rows < R) is updated as a row
     // vector (rhs_row_update32); with the quad tiles that row is a launch of its own (role 3,
     // outside the profiled scope: the roofline's launches are the quad and 128-row GEMMs)
-    const int rhs = R > c->nb ? c->nb : -1;
-    const bool quad = outer && pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb;
+    const int rhs = R > c->nb || jext > 0 ? c->nb : -1;
+    const bool quad =
+        outer && pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb && jext <= 0;
     {
         const int Rg = quad ? std::min(R, c->nb) : R;
         const double fl = c->prof ? update_flops(i0, Rg, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
@@ -485,7 +486,7 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
                                       c->h3ok, pl);
         } else if (outer) {
             // jext > jend: also the right-hand-side row's columns [jend, jext)
-            const auto sl = rhs >= 0 && jext > jend ? super_list_ext(c, i0, R, j0, jend, rhs, jext)
+            const auto sl = jext > jend ? super_list_ext(c, i0, R, j0, jend, rhs, jext)
                                                     : super_list(c, i0, R, j0, jend, Gap{0, 0}, rhs);
             launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
                                       c->h3_now ? c->nb : 0, c->h3ok, rhs, 0, pl);
@@ -495,7 +496,7 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
         }
         check_launch();
     }
-    if (quad && rhs >= 0) {
+    if (quad && R > c->nb) {
         const auto sl = super_list(c, c->nb, R, j0, jend, Gap{0, 0}, rhs);
         launch_chol_update32_t128(M, k0, kc, sl.first, sl.second, live_of(c), count, st, fd,
                                   c->nb, c->h3ok, rhs, 3, pl);
