@@ -1,0 +1,11 @@
+# Round-5 final record: GPU suite + smoke, round profile (kernel trace + PMC passes of the default
+# bench), the bench under the driver's invocation, the Newton-only PMC passes
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r05fin; mkdir -p $O
+bash tools/r05_gputests.sh > $O/tests.out 2>&1 || { echo "tests failed"; tail -20 $O/tests.out; exit 1; }
+tail -3 $O/tests.out
+bash tools/profile_round.sh > $O/profile_round.log 2>&1 || { echo "profile_round failed"; tail -20 $O/profile_round.log; exit 1; }
+echo "profile done"
+timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || { echo "bench failed"; tail -20 $O/bench20.err; exit 1; }
+echo "bench done"
+bash tools/r05_pmc_newton.sh > $O/pmc_newton.log 2>&1 || { echo "pmc newton failed"; tail -5 $O/pmc_newton.log; exit 1; }
+echo "pmc done"
