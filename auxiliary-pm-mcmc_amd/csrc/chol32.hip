@@ -1323,15 +1323,16 @@ __global__ __launch_bounds__(256) void k_zinv_step32(MatF A, int K, int m, int m
             }
 }
 
-// k_panel_inv_gemm32: workgroup (chain b, row tile i in [Kend, nb)) computes X_i = A_i Z^T for
-// the panel's 8 column tiles in fp16x3 (A_i split while staged, Z from its planes by LDS-DMA).
-// 8 waves: wave w takes rows 32 (w >> 2) .. +31 and column tiles w & 3 and 7 - (w & 3) (depths
-// (w & 3) + 1 and 8 - (w & 3) tiles: 9 each), two waves per SIMD so that one multiplies while
-// the other waits (one wave per SIMD left the loop exposed: 15 % MFMA busy). The workgroup reads
-// its row tile whole before it writes X_i in place (and the panel's planes for the trailing
-// update). 144 KB of LDS: one workgroup per CU.
+// k_panel_inv_gemm32: workgroup (chain b, row tiles i0 = Kend + 2p and i0 + 1) computes
+// X_i = A_i Z^T for the panel's 8 column tiles in fp16x3 (A_i split while staged, Z from its
+// planes by LDS-DMA). 8 waves: wave w takes row tile i0 + (w >> 2) and column tiles w & 3 and
+// 7 - (w & 3) (depths (w & 3) + 1 and 8 - (w & 3) tiles: 9 each), so every staged Z slice feeds
+// two row tiles (one row tile per workgroup staged Z per 64 output rows and left the loop waiting
+// on its slices: 15 - 17 % MFMA busy). The workgroup reads its row tiles whole before it writes
+// X in place (and the panel's planes for the trailing update). 160 KB of LDS: one workgroup per
+// CU, two waves per SIMD.
 struct __attribute__((aligned(16))) InvGemmSmem {
-    _Float16 a[2][2][64][LPH];   // [buffer][hi, lo][row][k] (HS layout)
+    _Float16 a[2][2][128][LPH];  // [buffer][hi, lo][row][k] (HS layout)
     _Float16 z[2][2][512][LPH];  // [buffer][hi, lo][Z row][k]
 };
 __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int Kend, int nb,
@@ -1340,30 +1341,38 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
                                                              const int* __restrict__ h3ok) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r16 = lane & 15, kq = lane >> 4;
     __shared__ InvGemmSmem sm;
-    const int nrows = nb - Kend;
-    const long w = xcd_remap32((long)blockIdx.x, (long)nrows * nchains);
-    const int b = (int)(w / nrows), i = Kend + (int)(w % nrows);
+    const int npair = (nb - Kend + 1) / 2;
+    const long w = xcd_remap32((long)blockIdx.x, (long)npair * nchains);
+    const int b = (int)(w / npair), i0 = Kend + 2 * (int)(w % npair);
+    const bool two = i0 + 1 < nb;  // (an odd count leaves the last workgroup one row tile)
     if (!live32(live, b) || (h3ok && !h3ok[b])) return;
-    float* Ai = A.base + b * A.cstride + (int64_t)(i * 64) * A.ld + K * 64;
-    const int rh = wv >> 2, c0 = wv & 3, c1 = 7 - (wv & 3);
-    f4_t acc0[2][4], acc1[2][4];
+    float* Ab = A.base + b * A.cstride + (int64_t)(i0 * 64) * A.ld + K * 64;
+    const int rt = wv >> 2, c0 = wv & 3, c1 = 7 - (wv & 3);
+    f4_t acc0[4][4], acc1[4][4];
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
         for (int bj = 0; bj < 4; ++bj) {
             acc0[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
             acc1[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
         }
-    // A staging: thread t moves row t/8, k 4(t%8) .. +3 of the 32-deep slice (split in registers)
-    const int arow = tid >> 3, acol = 4 * (tid & 7);
-    const float* ag = Ai + (int64_t)arow * A.ld + acol;
-    f4_t ra;
-    auto aload = [&](int sidx) { ra = *reinterpret_cast<const f4_t*>(ag + KS128 * sidx); };
+    // A staging: thread t moves row t/4 (of the two row tiles; a missing second tile re-reads the
+    // first), k 8(t%4) .. +7 of the 32-deep slice (split in registers)
+    const int arow = tid >> 2, acol = 8 * (tid & 3);
+    const float* ag = Ab + (int64_t)((two || arow < 64) ? arow : arow - 64) * A.ld + acol;
+    f4_t ra0, ra1;
+    auto aload = [&](int sidx) {
+        ra0 = *reinterpret_cast<const f4_t*>(ag + KS128 * sidx);
+        ra1 = *reinterpret_cast<const f4_t*>(ag + KS128 * sidx + 4);
+    };
     auto astore = [&](int buf) {
-        h4_t hi, lo;
-        split_h3(ra, hi, lo);
-        *reinterpret_cast<h4_t*>(&sm.a[buf][0][arow][HS(arow, acol)]) = hi;
-        *reinterpret_cast<h4_t*>(&sm.a[buf][1][arow][HS(arow, acol)]) = lo;
+        h4_t h0, l0, h1, l1;
+        split_h3(ra0, h0, l0);
+        split_h3(ra1, h1, l1);
+        const h8_t hi = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const h8_t lo = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        *reinterpret_cast<h8_t*>(&sm.a[buf][0][arow][HS(arow, acol)]) = hi;
+        *reinterpret_cast<h8_t*>(&sm.a[buf][1][arow][HS(arow, acol)]) = lo;
     };
     // Z staging by LDS-DMA: rows [64 kb, 512) of slice s (the column tiles that need it); wave
     // wv takes plane wv & 1 and the 16-row groups g = (wv >> 1) + 4t; lane l: row 16g + l/4,
@@ -1378,7 +1387,7 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
                 (glb_void_t*)(zg + ((int64_t)sidx * zpl.rows + 16 * g) * 32),
                 (lds_void_t*)&sm.z[buf][pln][16 * g][0], 16, 0, 0);
     };
-    auto mm = [&](f4_t (&acc)[2][4], int cc, int cur) {
+    auto mm = [&](f4_t (&acc)[4][4], int cc, int cur) {
         h8_t bh[4], bl[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
@@ -1387,8 +1396,8 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
             bl[x] = *reinterpret_cast<const h8_t*>(&sm.z[cur][1][row][HS(row, 8 * kq)]);
         }
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi) {
-            const int row = 32 * rh + 16 * bi + r16;
+        for (int bi = 0; bi < 4; ++bi) {
+            const int row = 64 * rt + 16 * bi + r16;
             const h8_t ah = *reinterpret_cast<const h8_t*>(&sm.a[cur][0][row][HS(row, 8 * kq)]);
             const h8_t al = *reinterpret_cast<const h8_t*>(&sm.a[cur][1][row][HS(row, 8 * kq)]);
 #pragma unroll
@@ -1399,6 +1408,7 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
             }
         }
     };
+    const bool mine = two || rt == 0;  // a missing second row tile: its waves only stage
     constexpr int nsub = 512 / KS128;
     aload(0);
     dma(0, 0);
@@ -1411,24 +1421,26 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
             dma(s + 1, (s + 1) & 1);
         }
         const int kb = s >> 1;
-        if (kb <= c0) mm(acc0, c0, s & 1);
-        if (kb <= c1) mm(acc1, c1, s & 1);
+        if (mine && kb <= c0) mm(acc0, c0, s & 1);
+        if (mine && kb <= c1) mm(acc1, c1, s & 1);
         if (s + 1 < nsub) astore((s + 1) & 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    // X_i in place (the whole row tile was read above) and the panel's planes
+    if (!mine) return;
+    // X in place (both row tiles were read whole above) and the panel's planes
+    const int i = i0 + rt;
+    float* Ai = Ab + (int64_t)(rt * 64) * A.ld;
     const bool planes = pl.base && (i + 1) * 64 <= pl.rows;
-    auto put = [&](const f4_t (&acc)[2][4], int cc) {
+    auto put = [&](const f4_t (&acc)[4][4], int cc) {
         unsigned short* hp = planes ? pl.base + b * pl.cstride : nullptr;
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+        for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
             for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int rr = 32 * rh + 16 * bi + F32_CROW(lane, r);
-                    const int col = 64 * cc + 16 * bj + r16;
+                    const int rr = 16 * bi + F32_CROW(lane, r), col = 64 * cc + 16 * bj + r16;
                     const float v = acc[bi][bj][r];
                     Ai[(int64_t)rr * A.ld + col] = v;
                     if (planes) {
@@ -1455,8 +1467,9 @@ void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstrid
                                A, K, m, mode, zt, zstride, zpl, live, h3ok);
     const int Kend = K + 8;
     if (nb > Kend)
-        hipLaunchKernelGGL(k_panel_inv_gemm32, dim3((unsigned)((long)(nb - Kend) * nchains)),
-                           dim3(512), 0, s, A, K, Kend, nb, zpl, pl, live, nchains, h3ok);
+        hipLaunchKernelGGL(k_panel_inv_gemm32,
+                           dim3((unsigned)((long)((nb - Kend + 1) / 2) * nchains)), dim3(512), 0,
+                           s, A, K, Kend, nb, zpl, pl, live, nchains, h3ok);
 }
 
 // Host: 256x256 quad tiles covering tiles (i, j), i in [i0, R), j0 <= j <= min(i, jend-1), in
