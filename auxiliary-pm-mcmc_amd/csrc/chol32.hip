@@ -1239,8 +1239,7 @@ void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, in
 //
 // Z = inv(L_D) by recursive doubling in 64-tile units (fp32 MFMA): with L_D split into
 // [[L11, 0], [L21, L22]] of m x m tiles, Z21 = -Z22 (L21 Z11). Level m = 1, 2, 4 takes the
-// 8 / (2m) diagonal pairs of the level at once, each in two batched tile-product launches
-// (T = L21 Z11, then Z21 = -Z22 T), so Z needs 1 + 3 x 2 dependent launches of 64x64 tile
+// 8 / (2m) diagonal pairs of the level at once, so Z needs 3 dependent launches of 64x64 tile
 // products (depth <= 4 tiles) instead of a 7-step substitution per column (150-270 us per panel
 // at 64 chains, round 5). Scratch per chain (zt, 3 x 512 x 512 fp32): Z row-major, Z^T, and T^T,
 // the operands of tile_gemm_nt32's A B^T form; Z also goes out as fp16x3 planes (512 rows).
@@ -1252,35 +1251,29 @@ __device__ __forceinline__ void zput16(unsigned short* Z, const Planes16& zp, in
     Z[o + zp.lo] = __builtin_bit_cast(unsigned short, l);
 }
 #define ZS 512  // scratch leading dimension
-// diagonal tiles: Z_ii = inv(L_ii) (row-major in Dinv)
-__global__ __launch_bounds__(256) void k_zinv_diag32(int K, const float* __restrict__ Dinv,
-                                                     int64_t dstride, float* zt, int64_t zstride,
-                                                     Planes16 zpl, Live live,
-                                                     const int* __restrict__ h3ok) {
-    const int b = blockIdx.x >> 3, i = blockIdx.x & 7;
-    if (!live32(live, b) || (h3ok && !h3ok[b])) return;
-    float* Zr = zt + b * zstride;
-    float* ZT = Zr + ZS * ZS;
-    unsigned short* Zp = zpl.base + b * zpl.cstride;
-    const float* D = Dinv + b * dstride + (int64_t)(K + i) * 4096;
-    for (int e = threadIdx.x; e < 4096; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        const float v = D[e];
-        Zr[(int64_t)(64 * i + r) * ZS + 64 * i + c] = v;
-        ZT[(int64_t)(64 * i + c) * ZS + 64 * i + r] = v;
-        zput16(Zp, zpl, 64 * i + r, 64 * i + c, v);
+// one level m of the doubling: workgroup (chain, pair p, column tb) of the pair whose L21 sits at
+// tile rows r0 = 2mp + m, columns c0 = 2mp computes column tb of T = L21 Z11 (stored transposed),
+// then column tb of Z21 = -Z22 T (stored as Z, Z^T and planes); level 1 first writes the pair's
+// two diagonal tiles Z_ii = inv(L_ii). Three launches per panel (m = 1, 2, 4: 4 workgroups per
+// chain each) - the stages were 7 launches, each waiting for CU slots behind the far update
+// (~60 us apiece there against ~15 alone)
+__device__ __forceinline__ void own_stores_visible() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __syncthreads();
 }
-// one stage of level m: workgroup (chain, pair p, output tile (a, b)) of the pair whose L21 sits at
-// tile rows r0 = 2mp + m, columns c0 = 2mp. mode 0: T_ab = sum_{k=b}^{m-1} L21_ak Z11_kb, stored
-// transposed; mode 1: Z21_ab = -sum_{k=0}^{a} Z22_ak T_kb, stored as Z, Z^T and planes
-__global__ __launch_bounds__(256) void k_zinv_step32(MatF A, int K, int m, int mode, float* zt,
-                                                     int64_t zstride, Planes16 zpl, Live live,
-                                                     const int* __restrict__ h3ok) {
-    const int per = 4 / m * m * m;  // output tiles per chain: (8 / 2m) pairs x m x m
-    const int b = blockIdx.x / per, w = blockIdx.x % per;
+__global__ __launch_bounds__(256) void k_zinv_level32(MatF A, int K, int m,
+                                                      const float* __restrict__ Dinv,
+                                                      int64_t dstride, float* zt, int64_t zstride,
+                                                      Planes16 zpl, Live live,
+                                                      const int* __restrict__ h3ok) {
+    const int b = blockIdx.x >> 2, w = blockIdx.x & 3;
     if (!live32(live, b) || (h3ok && !h3ok[b])) return;
-    const int p = w / (m * m), ta = (w % (m * m)) / m, tb = w % m;
+    const int p = w / m, tb = w % m;
     const int r0 = 2 * m * p + m, c0 = 2 * m * p;
     __shared__ GemmSmem32 sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wr = wv >> 1, wc = wv & 1;
@@ -1288,39 +1281,66 @@ __global__ __launch_bounds__(256) void k_zinv_step32(MatF A, int K, int m, int m
     float* Zr = zt + b * zstride;
     float* ZT = Zr + ZS * ZS;
     float* Tt = ZT + ZS * ZS;
-    f4_t acc[2][2];
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
-    if (mode == 0) {
-        const float* L = A.base + b * A.cstride + (int64_t)((K + r0 + ta) * 64) * A.ld +
-                         (K + c0 + tb) * 64;
-        tile_gemm_nt32<false>(acc, L, A.ld, ZT + (int64_t)((c0 + tb) * 64) * ZS + (c0 + tb) * 64,
-                              ZS, 64 * (m - tb), sm, nullptr, 0);
-    } else {
-        tile_gemm_nt32<true>(acc, Zr + (int64_t)((r0 + ta) * 64) * ZS + r0 * 64, ZS,
-                             Tt + (int64_t)((c0 + tb) * 64) * ZS + r0 * 64, ZS, 64 * (ta + 1),
-                             sm, nullptr, 0);
-    }
     unsigned short* Zp = zpl.base + b * zpl.cstride;
+    const float* Ab = A.base + b * A.cstride;
+    if (m == 1) {  // the pair's diagonal tiles (row-major inverses in Dinv)
+        for (int q = 0; q < 2; ++q) {
+            const int t = c0 + q;
+            const float* D = Dinv + b * dstride + (int64_t)(K + t) * 4096;
+            for (int e = tid; e < 4096; e += 256) {
+                const int r = e >> 6, c = e & 63;
+                const float v = D[e];
+                Zr[(int64_t)(64 * t + r) * ZS + 64 * t + c] = v;
+                ZT[(int64_t)(64 * t + c) * ZS + 64 * t + r] = v;
+                zput16(Zp, zpl, 64 * t + r, 64 * t + c, v);
+            }
+        }
+        own_stores_visible();
+    }
+    f4_t acc[2][2];
+    auto zero = [&]() {
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+        for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
+            for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = f4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    // column tb of T: T_a,tb = sum_{k=tb}^{m-1} L21_ak Z11_k,tb
+    for (int ta = 0; ta < m; ++ta) {
+        zero();
+        tile_gemm_nt32<false>(acc, Ab + (int64_t)((K + r0 + ta) * 64) * A.ld + (K + c0 + tb) * 64,
+                              A.ld, ZT + (int64_t)((c0 + tb) * 64) * ZS + (c0 + tb) * 64, ZS,
+                              64 * (m - tb), sm, nullptr, 0);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
-                const float v = acc[bi][bj][r];
-                const int zr = (r0 + ta) * 64 + rr, zc = (c0 + tb) * 64 + cc;
-                if (mode == 0) {
-                    Tt[(int64_t)zc * ZS + zr] = v;
-                } else {
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
+                    Tt[(int64_t)((c0 + tb) * 64 + cc) * ZS + (r0 + ta) * 64 + rr] = acc[bi][bj][r];
+                }
+    }
+    own_stores_visible();
+    // column tb of Z21: Z21_a,tb = -sum_{k=0}^{a} Z22_ak T_k,tb
+    for (int ta = 0; ta < m; ++ta) {
+        zero();
+        tile_gemm_nt32<true>(acc, Zr + (int64_t)((r0 + ta) * 64) * ZS + r0 * 64, ZS,
+                             Tt + (int64_t)((c0 + tb) * 64) * ZS + r0 * 64, ZS, 64 * (ta + 1), sm,
+                             nullptr, 0);
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = 32 * wr + 16 * bi + F32_CROW(lane, r), cc = 32 * wc + 16 * bj + r16;
+                    const float v = acc[bi][bj][r];
+                    const int zr = (r0 + ta) * 64 + rr, zc = (c0 + tb) * 64 + cc;
                     Zr[(int64_t)zr * ZS + zc] = v;
                     ZT[(int64_t)zc * ZS + zr] = v;
                     zput16(Zp, zpl, zr, zc, v);
                 }
-            }
+    }
 }
 
 // k_panel_inv_gemm32: workgroup (chain b, row tiles i0 = Kend + 2p and i0 + 1) computes
@@ -1459,12 +1479,9 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
 void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
                         int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
                         const int* h3ok, hipStream_t s) {
-    hipLaunchKernelGGL(k_zinv_diag32, dim3((unsigned)(8 * nchains)), dim3(256), 0, s, K, Dinv,
-                       dstride, zt, zstride, zpl, live, h3ok);
     for (int m = 1; m <= 4; m *= 2)
-        for (int mode = 0; mode < 2; ++mode)
-            hipLaunchKernelGGL(k_zinv_step32, dim3((unsigned)(4 * m * nchains)), dim3(256), 0, s,
-                               A, K, m, mode, zt, zstride, zpl, live, h3ok);
+        hipLaunchKernelGGL(k_zinv_level32, dim3((unsigned)(4 * nchains)), dim3(256), 0, s, A, K,
+                           m, Dinv, dstride, zt, zstride, zpl, live, h3ok);
     const int Kend = K + 8;
     if (nb > Kend)
         hipLaunchKernelGGL(k_panel_inv_gemm32,
