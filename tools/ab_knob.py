@@ -56,12 +56,13 @@ def main():
                 ('CHOL_UPDATE32_OUTER', 'CHOL_UPDATE_OUTER', 'UGEMM', 'POST32_OUTER')}
         ctrs = [ctx.prof_read(k)[1] for k in (_native.PROF_STATS, _native.PROF_DF_TIMEOUTS,
                                                _native.PROF_TRSV_TIMEOUTS)]
+        nref = ctx.prof_read(_native.PROF_STATS)[2] / a.reps  # refinement rounds per theta-call
         ctx.close()
         h = hashlib.sha1(out.tobytes()).hexdigest()[:12]
         line = '{0}={1}: theta-call {2:.2f} ms (min {3:.2f})  u-call {4:.3f} ms  hash {5}  ' \
-               'status ok {6}  reruns/df/trsv timeouts {7}'.format(
+               'status ok {6}  reruns/df/trsv timeouts {7}  refinement rounds {8:.1f}'.format(
                    a.var, v, 1e3 * np.median(ts), 1e3 * min(ts), 1e3 * np.median(tu), h,
-                   bool((st == 0).all() and (st2 == 0).all()), ctrs)
+                   bool((st == 0).all() and (st2 == 0).all()), ctrs, nref)
         if base is None:
             base = (out, out2, nops)
         else:
