@@ -155,7 +155,7 @@ std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, i
 // also forms the fp32 Newton matrix I + W^1/2 K W^1/2 and its right-hand-side block (x = b)
 void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,
                  double* part, int64_t pstride, int np, MatF Bf, const double* Ws,
-                 int64_t wstride, Live live, int nchains, hipStream_t s);
+                 int64_t wstride, Live live, int nchains, hipStream_t s, int symv_tpw = 1);
 void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Live live,
                   int nchains, hipStream_t s);
 // blocked TRSV steps with fp32 tiles / inverses and fp64 vectors (r updated in place)

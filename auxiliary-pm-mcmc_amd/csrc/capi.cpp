@@ -125,6 +125,7 @@ struct apm_ctx {
     // dataflow launch walks the diagonal block and the right-hand-side row only; Z = inv(L_D) per
     // chain (fp32 scratch zt: Z, Z^T, T^T; fp16x3 planes zplanes) and one GEMM per row tile below
     bool dfinv = true;
+    int symv_tpw = 2;  // K x: lower tiles per workgroup (APM_SYMV_TPW: 1, 2 or 4)
     float* zt = nullptr;
     unsigned short* zplanes = nullptr;
     // per (chain, row tile) progress words, then [dataflow timeouts][TRSV timeouts][ticket]
@@ -707,7 +708,7 @@ void newton_solve32(apm_ctx* c, int count) {
         launch_refine(0, c->v.Ws, c->v.Kb, c->v.z, nullptr, r2, vs, np, lr, count, s);  // t
         check_launch();
         launch_symv(c->K, r2, vs, r3, vs, c->sympart, c->sstride, np, MatF{}, nullptr, 0, lr,
-                    count, s);                                                           // K t
+                    count, s, c->symv_tpw);  // K t
         check_launch();
         launch_refine(1, c->v.Ws, c->v.Kb, c->v.z, r3, r1, vs, np, lr, count, s);       // res
         check_launch();
@@ -756,13 +757,14 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         check_launch();
         if (mixed) {  // K b and the fp32 B (+ its right-hand side) in one pass over K's lower half
             launch_symv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->sympart, c->sstride,
-                        c->np, b32_of(c), c->v.Ws, c->v.vstride, lv, count, c->stream);
+                        c->np, b32_of(c), c->v.Ws, c->v.vstride, lv, count, c->stream,
+                        c->symv_tpw);
         } else if (c->k_full) {
             launch_gemv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->np, lv, count,
                         c->stream);
         } else {
             launch_symv(c->K, c->v.b, c->v.vstride, c->v.Kb, c->v.vstride, c->sympart, c->sstride,
-                        c->np, MatF{}, nullptr, 0, lv, count, c->stream);
+                        c->np, MatF{}, nullptr, 0, lv, count, c->stream, c->symv_tpw);
         }
         check_launch();
         if (mixed) {
@@ -781,7 +783,7 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         check_launch();
         if (mixed || !c->k_full)
             launch_symv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->sympart,
-                        c->sstride, c->np, MatF{}, nullptr, 0, lv, count, c->stream);
+                        c->sstride, c->np, MatF{}, nullptr, 0, lv, count, c->stream, c->symv_tpw);
         else
             launch_gemv(c->K, c->v.a, c->v.vstride, c->v.fnew, c->v.vstride, c->np, lv, count,
                         c->stream);
@@ -1248,6 +1250,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_PLANES")) c->planes_on = atoi(e) != 0;
     if (const char* e = getenv("APM_Q256")) c->q256 = atoi(e) != 0;
     if (const char* e = getenv("APM_DFINV")) c->dfinv = atoi(e) != 0;
+    if (const char* e = getenv("APM_SYMV_TPW")) c->symv_tpw = atoi(e);
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));

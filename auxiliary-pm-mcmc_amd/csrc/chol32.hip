@@ -1576,6 +1576,15 @@ void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Li
 // part[tj][ti]; k_symv_reduce adds the nb partials of every row in a fixed order (deterministic,
 // no atomics). With `Bf` set, the same pass also writes the fp32 Newton matrix tile
 // I + W^1/2 K W^1/2 (fusing k_form_B32 into the x = b pass).
+// TPW > 1: a workgroup takes TPW consecutive tiles of its chain, the next tile's 32 KB loaded
+// into registers while the current one is reduced (the same per-tile sums: bitwise equal)
+__device__ __forceinline__ void symv_tile_ij(int t, int& ti, int& tj) {
+    ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > t) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    tj = t - ti * (ti + 1) / 2;
+}
+template <int TPW>
 __global__ __launch_bounds__(256) void k_symv_part(MatB K, const double* __restrict__ x,
                                                    int64_t xstride, double* __restrict__ part,
                                                    int64_t pstride, int nb, MatF Bf,
@@ -1583,82 +1592,103 @@ __global__ __launch_bounds__(256) void k_symv_part(MatB K, const double* __restr
                                                    Live live) {
     const int b = blockIdx.y;
     if (!live32(live, b)) return;
-    const int t = blockIdx.x;
-    int ti = (int)floor((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (ti * (ti + 1) / 2 > t) --ti;
-    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-    const int tj = t - ti * (ti + 1) / 2;
+    const int ntile = nb * (nb + 1) / 2;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int rg = tid >> 4, cg = tid & 15;  // rows 4rg .. 4rg+3, columns 4cg .. 4cg+3
-    const double* Kt = K.base + b * K.cstride + (int64_t)(ti * 64 + 4 * rg) * K.ld + tj * 64 + 4 * cg;
-    d2_t v[4][2];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        v[r][0] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld);
-        v[r][1] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld + 2);
-    }
-    const double* xb = x + b * xstride;
-    const d2_t xj0 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg);
-    const d2_t xj1 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg + 2);
-    const d2_t xi0 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg);
-    const d2_t xi1 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg + 2);
-    const double xjv[4] = {xj0.x, xj0.y, xj1.x, xj1.y}, xiv[4] = {xi0.x, xi0.y, xi1.x, xi1.y};
-    if (Bf.base) {
-        const double* wb = Ws + b * wstride;
-        float* Fb = Bf.base + b * Bf.cstride + (int64_t)(ti * 64 + 4 * rg) * Bf.ld + tj * 64 + 4 * cg;
-        const int gr0 = ti * 64 + 4 * rg, gc0 = tj * 64 + 4 * cg;
-        const d2_t wc0 = *reinterpret_cast<const d2_t*>(wb + gc0);
-        const d2_t wc1 = *reinterpret_cast<const d2_t*>(wb + gc0 + 2);
-        const double wcv[4] = {wc0.x, wc0.y, wc1.x, wc1.y};
+    __shared__ double cs[4][64];
+    auto load = [&](int t, d2_t (&v)[4][2]) {
+        int ti, tj;
+        symv_tile_ij(t, ti, tj);
+        const double* Kt =
+            K.base + b * K.cstride + (int64_t)(ti * 64 + 4 * rg) * K.ld + tj * 64 + 4 * cg;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const double wr_ = wb[gr0 + r];
-            const double kv[4] = {v[r][0].x, v[r][0].y, v[r][1].x, v[r][1].y};
-            f4_t o;
+            v[r][0] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld);
+            v[r][1] = *reinterpret_cast<const d2_t*>(Kt + (int64_t)r * K.ld + 2);
+        }
+    };
+    int t = blockIdx.x * TPW;
+    d2_t v[4][2];
+    load(t, v);
+    for (int tt = 0; tt < TPW && t < ntile; ++tt, ++t) {
+        d2_t vn[4][2];
+        if (TPW > 1 && tt + 1 < TPW && t + 1 < ntile) load(t + 1, vn);
+        int ti, tj;
+        symv_tile_ij(t, ti, tj);
+        const double* xb = x + b * xstride;
+        const d2_t xj0 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg);
+        const d2_t xj1 = *reinterpret_cast<const d2_t*>(xb + tj * 64 + 4 * cg + 2);
+        const d2_t xi0 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg);
+        const d2_t xi1 = *reinterpret_cast<const d2_t*>(xb + ti * 64 + 4 * rg + 2);
+        const double xjv[4] = {xj0.x, xj0.y, xj1.x, xj1.y}, xiv[4] = {xi0.x, xi0.y, xi1.x, xi1.y};
+        if (Bf.base) {
+            const double* wb = Ws + b * wstride;
+            float* Fb = Bf.base + b * Bf.cstride + (int64_t)(ti * 64 + 4 * rg) * Bf.ld + tj * 64 +
+                        4 * cg;
+            const int gr0 = ti * 64 + 4 * rg, gc0 = tj * 64 + 4 * cg;
+            const d2_t wc0 = *reinterpret_cast<const d2_t*>(wb + gc0);
+            const d2_t wc1 = *reinterpret_cast<const d2_t*>(wb + gc0 + 2);
+            const double wcv[4] = {wc0.x, wc0.y, wc1.x, wc1.y};
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                o[c] = (float)((gr0 + r == gc0 + c ? 1.0 : 0.0) + (wr_ * kv[c]) * wcv[c]);
-            *reinterpret_cast<f4_t*>(Fb + (int64_t)r * Bf.ld) = o;
+            for (int r = 0; r < 4; ++r) {
+                const double wr_ = wb[gr0 + r];
+                const double kv[4] = {v[r][0].x, v[r][0].y, v[r][1].x, v[r][1].y};
+                f4_t o;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    o[c] = (float)((gr0 + r == gc0 + c ? 1.0 : 0.0) + (wr_ * kv[c]) * wcv[c]);
+                *reinterpret_cast<f4_t*>(Fb + (int64_t)r * Bf.ld) = o;
+            }
+        }
+        double* pb = part + b * pstride;
+        // row sums over this thread's 4 columns, then over the 16 lanes of the row group
+        double rs[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double sr = v[r][0].x * xjv[0];
+            sr = fma(v[r][0].y, xjv[1], sr);
+            sr = fma(v[r][1].x, xjv[2], sr);
+            sr = fma(v[r][1].y, xjv[3], sr);
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
+            rs[r] = sr;
+        }
+        if (cg < 4) pb[((int64_t)ti * nb + tj) * 64 + 4 * rg + cg] = rs[cg];
+        if (ti != tj) {  // (uniform per workgroup)
+            // column sums over this thread's 4 rows, then over the 4 row groups of the wave and
+            // the 4 waves
+            double csum[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const double kc0 = c < 2 ? (c == 0 ? v[0][0].x : v[0][0].y) : (c == 2 ? v[0][1].x : v[0][1].y);
+                const double kc1 = c < 2 ? (c == 0 ? v[1][0].x : v[1][0].y) : (c == 2 ? v[1][1].x : v[1][1].y);
+                const double kc2 = c < 2 ? (c == 0 ? v[2][0].x : v[2][0].y) : (c == 2 ? v[2][1].x : v[2][1].y);
+                const double kc3 = c < 2 ? (c == 0 ? v[3][0].x : v[3][0].y) : (c == 2 ? v[3][1].x : v[3][1].y);
+                double sc = kc0 * xiv[0];
+                sc = fma(kc1, xiv[1], sc);
+                sc = fma(kc2, xiv[2], sc);
+                sc = fma(kc3, xiv[3], sc);
+                sc += __shfl_xor(sc, 16, 64);
+                sc += __shfl_xor(sc, 32, 64);
+                csum[c] = sc;
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) cs[w][4 * lane + c] = csum[c];
+            }
+            __syncthreads();
+            if (tid < 64)
+                pb[((int64_t)tj * nb + ti) * 64 + tid] = cs[0][tid] + cs[1][tid] + cs[2][tid] + cs[3][tid];
+            if (TPW > 1) __syncthreads();  // cs is rewritten by the next tile
+        }
+        if (TPW > 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r][0] = vn[r][0];
+                v[r][1] = vn[r][1];
+            }
         }
     }
-    double* pb = part + b * pstride;
-    // row sums over this thread's 4 columns, then over the 16 lanes of the row group
-    double rs[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        double sr = v[r][0].x * xjv[0];
-        sr = fma(v[r][0].y, xjv[1], sr);
-        sr = fma(v[r][1].x, xjv[2], sr);
-        sr = fma(v[r][1].y, xjv[3], sr);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
-        rs[r] = sr;
-    }
-    if (cg < 4) pb[((int64_t)ti * nb + tj) * 64 + 4 * rg + cg] = rs[cg];
-    if (ti == tj) return;  // uniform per workgroup
-    // column sums over this thread's 4 rows, then over the 4 row groups of the wave and 4 waves
-    __shared__ double cs[4][64];
-    double csum[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const double kc0 = c < 2 ? (c == 0 ? v[0][0].x : v[0][0].y) : (c == 2 ? v[0][1].x : v[0][1].y);
-        const double kc1 = c < 2 ? (c == 0 ? v[1][0].x : v[1][0].y) : (c == 2 ? v[1][1].x : v[1][1].y);
-        const double kc2 = c < 2 ? (c == 0 ? v[2][0].x : v[2][0].y) : (c == 2 ? v[2][1].x : v[2][1].y);
-        const double kc3 = c < 2 ? (c == 0 ? v[3][0].x : v[3][0].y) : (c == 2 ? v[3][1].x : v[3][1].y);
-        double sc = kc0 * xiv[0];
-        sc = fma(kc1, xiv[1], sc);
-        sc = fma(kc2, xiv[2], sc);
-        sc = fma(kc3, xiv[3], sc);
-        sc += __shfl_xor(sc, 16, 64);
-        sc += __shfl_xor(sc, 32, 64);
-        csum[c] = sc;
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) cs[w][4 * lane + c] = csum[c];
-    }
-    __syncthreads();
-    if (tid < 64) pb[((int64_t)tj * nb + ti) * 64 + tid] = cs[0][tid] + cs[1][tid] + cs[2][tid] + cs[3][tid];
 }
 
 // y[i] = sum_tj part[i/64][tj][i%64]; with Bf: also the Newton right-hand-side block of the fp32
@@ -1686,10 +1716,17 @@ __global__ __launch_bounds__(256) void k_symv_reduce(const double* __restrict__ 
 
 void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ystride,
                  double* part, int64_t pstride, int np, MatF Bf, const double* Ws,
-                 int64_t wstride, Live live, int nchains, hipStream_t s) {
-    const int nb = np / 64;
-    hipLaunchKernelGGL(k_symv_part, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, K, x,
-                       xstride, part, pstride, nb, Bf, Ws, wstride, live);
+                 int64_t wstride, Live live, int nchains, hipStream_t s, int symv_tpw) {
+    const int nb = np / 64, nt = nb * (nb + 1) / 2;
+    if (symv_tpw >= 4)
+        hipLaunchKernelGGL(k_symv_part<4>, dim3((nt + 3) / 4, nchains), dim3(256), 0, s, K, x,
+                           xstride, part, pstride, nb, Bf, Ws, wstride, live);
+    else if (symv_tpw == 2)
+        hipLaunchKernelGGL(k_symv_part<2>, dim3((nt + 1) / 2, nchains), dim3(256), 0, s, K, x,
+                           xstride, part, pstride, nb, Bf, Ws, wstride, live);
+    else
+        hipLaunchKernelGGL(k_symv_part<1>, dim3(nt, nchains), dim3(256), 0, s, K, x, xstride,
+                           part, pstride, nb, Bf, Ws, wstride, live);
     hipLaunchKernelGGL(k_symv_reduce, dim3((np + 255) / 256, nchains), dim3(256), 0, s, part,
                        pstride, nb, y, ystride, Bf, Ws, wstride, live);
 }

@@ -172,6 +172,29 @@ def test_config4_full_size_paths_agree(nat, monkeypatch):
                                        atol=2e-8 * np.abs(ref[4][b]).max())
 
 
+def test_config2_stationary_states_match_fp64_newton(nat, monkeypatch):
+    """The regime the bench's headline is timed in: configs[2] (N=4096 D=32 N_imp=256) at 8 of
+    the long-chain record's stationary chain states (tests/golden/stationary_thetas.npy, a copy
+    of profiles/r04_stationary_thetas.npy: log sigma 3.1-4.3, 7-8 Newton iterations, two
+    refinement rounds per iteration), the default mixed-precision path (fp16x3 explicit-inverse
+    panels, fp32 posterior bottom block) against the all-fp64 Newton iteration (APM_MIXED=0) on
+    the same (theta, u): estimates within TOL_NATS, n_cubic_ops equal, f_post within FPOST_REL
+    (measured 5.5e-11 over 16 chains, profiles/r05_refine_tol_study.txt)."""
+    from gpdemo.utils import synthetic_gp_data
+    X, y = synthetic_gp_data(4096, 32, 20151009)
+    th = np.load(os.path.join(os.path.dirname(__file__), 'golden',
+                              'stationary_thetas.npy'))[::8].astype(np.float64)
+    U = np.random.RandomState(5).normal(size=(4096, 256))
+    ref = _run(nat, X, y, th, 256, U, monkeypatch, APM_MIXED=0)
+    o, st, nops, o2, f = _run(nat, X, y, th, 256, U, monkeypatch)
+    assert (ref[1] == 0).all() and (st == 0).all()
+    np.testing.assert_array_equal(nops, ref[2])
+    for b in range(th.shape[0]):
+        assert abs(o[b] - ref[0][b]) <= TOL_NATS, b
+        assert abs(o2[b] - ref[3][b]) <= TOL_NATS, b
+        assert np.abs(f[b] - ref[4][b]).max() <= FPOST_REL * np.abs(ref[4][b]).max(), b
+
+
 def test_config0_pmmh_chain_matches_reference(nat):
     import auxpm.samplers as smp
     import gpdemo.estimators as est
