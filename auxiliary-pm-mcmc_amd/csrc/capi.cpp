@@ -1052,6 +1052,10 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     const bool syrk1 = nb >= 2;
     launch_form_y2_rev(BL, TL, np, c->v.Ws, vs, np, lv, count, s, !syrk1);  // Y2, Y = L_K J
     check_launch();
+    // the bottom block's fp32 copy of L_K J (stream2, HBM-bound) beside the SYRK (MFMA-bound)
+    // rather than beside the first panel's latency-bound in-panel steps (-1.4 ms per stationary
+    // theta-call, profiles/r05_conv_early_ab.txt)
+    if (c->post32 == 2) post_bottom32_begin(c, count);
     if (syrk1) {
         tracked_update(c, TL, nb, nb, 0, nb, 0, nb, Gap{0, 0}, 2, count);
     } else {
@@ -1067,7 +1071,6 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     } else if (c->post32 == 1) {  // J M J alone in fp64 (its log-determinant is log|B|)
         chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count);
     } else {  // ... with the fp32 bottom block following its panels on stream2
-        post_bottom32_begin(c, count);
         chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count, true, 0, no_gap, nullptr,
                    nullptr, [c, count](int K, int Kend) { post_bottom32_panel(c, count, K, Kend); });
     }
