@@ -1,5 +1,5 @@
-# Round-5 A/B batch 1 on one MI355X: the stationary bench with 1 and 2 cohorts per GPU (short,
-# no CPU baseline / parity / ESS extension), then the APM_GEMM A/B (tools/r05_gemm.sh).
+# Round-5 A/B on one MI355X: the stationary bench with 1 and 2 cohorts per GPU (short, no CPU
+# baseline / parity / ESS extension)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r05c; mkdir -p $O
 for K in 1 2 1 2; do
   timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --cpu-baseline 0 --parity 0 --ess-min 0 --ess-burn 0 --cohorts $K > $O/coh$K.json 2> $O/coh$K.err || exit $?
