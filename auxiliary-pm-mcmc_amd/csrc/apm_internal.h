@@ -213,7 +213,7 @@ void launch_newton_check(NewtonVecs v, int n, int np, double tol, int* active, c
                          int* n_iter, int nchains, hipStream_t s);
 void launch_copy_lower(MatB src, MatB dst, int np, Live live, int nchains, hipStream_t s);
 void launch_form_aug(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains,
-                     hipStream_t s);
+                     hipStream_t s, bool lower_only = false);
 // per chain: out[b] = -0.5 a.f + sum_n log_ndtr(y f) - 0.5*sum(ldet[0..nb))*2
 void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet,
                         int64_t lstride, int nb, double* out, Live live, int nchains,
@@ -238,6 +238,8 @@ struct SlotSet {
     double wide_q;      // the threshold (APM_WIDE_Q, overridable by the environment variable)
     double post_q;      // trace(C) above which an fp32 bottom block is recomputed in fp64
                         // (APM_POST32_Q; postcov.hip)
+    const double* icm_thr;  // per chain: trace(C) below which bit 3 of chain_wide asks the host
+                            // for the reference-route check of chol(C) (capi.cpp icm_check)
 };
 // trace(L L^T) above which a slot's u-path runs in fp64: the fp32 L.U moves
 // log f by ~1e-10 x trace (11 nats at trace 1.15e11, sigma = e^18.5; < 1e-6 nats at the trace

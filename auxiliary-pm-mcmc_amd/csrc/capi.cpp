@@ -31,6 +31,11 @@ struct ProfRec {
     double work;
 };
 
+// per chain: the trace(C) below which the reference's route to chol(C) is checked (icm_check):
+// C's mean diagonal below APM_ICM_Q^-1 of K's largest diagonal entry, i.e. K - V^T V cancels
+// ~log10(APM_ICM_Q) digits or more (1e-7 of K_ii at the golden ICM theta icm_a, 1e-5 at icm_b;
+// ~1/4 at configs[2]'s sigma = e^18.5, and no chain of the bench's stationary states: unchecked)
+#define APM_ICM_Q 1.0e3
 struct apm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -66,6 +71,11 @@ struct apm_ctx {
     int* refining = nullptr;  // chains still refining their Newton solve
     double* refine_prev = nullptr;  // max|d| of the previous refinement step per chain
     int64_t n_refine_steps = 0, n_fp64_rerun = 0;  // statistics (apm_prof_read APM_PROF_STATS)
+    int64_t n_icm_check = 0;  // chains whose C was formed the reference's way (icm_check)
+    // APM_ICM=0: no check of the reference's chol(C) (icm_check); APM_ICM_Q: its threshold
+    // (development knob: a huge value checks every chain)
+    bool icm = true;
+    double icm_q = APM_ICM_Q;
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;  // d_ubufs = d_slots + B
     // pinned host staging of the per-call uploads (one H2D of slots + ubufs; the per-chain
     // fp16x3 flags): [B slots][B ubufs][B h3ok]
@@ -105,6 +115,7 @@ struct apm_ctx {
     bool q256 = true;
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
     int* h3post = nullptr;  // the same for the posterior factor's fp32 bottom block (h3ok + B)
+    double* icm_thr = nullptr;  // per chain: SlotSet::icm_thr
     // the bottom block of the posterior factor [[J M J],[L_K J]] (the TRSM that yields chol(C) J)
     // in fp32 after the fp64 factorisation of J M J (postcov.hip; APM_POST32=0: all fp64); chains
     // whose trace(C) exceeds Sl.post_q are recomputed in fp64 (n_post64 counts them)
@@ -639,6 +650,7 @@ void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubuf
 }
 int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 16 * c->max_batch); }
 int* pin_h3post(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 20 * c->max_batch); }
+double* pin_icm(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 24 * c->max_batch); }
 
 // per-chain fp16x3 flags of a theta-call -> device (chol32.hip: |L_ij| <= sqrt(1 + K_ii) must
 // stay below fp16's range); h3_now = any chain flagged (else the fp32-operand kernel launches)
@@ -653,6 +665,9 @@ void upload_h3(apm_ctx* c, int count) {
     HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->h3post, pin_h3post(c), sizeof(int) * count, hipMemcpyHostToDevice,
                         c->stream));
+    double* t = pin_icm(c);
+    for (int b = 0; b < count; ++b) t[b] = c->icm ? t[b] : -1.0;
+    HIPC(hipMemcpyAsync(c->icm_thr, t, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
 }
 
 // wide: some slot of the call may be wide (theta-calls: unknown until the read-back; u-calls:
@@ -1004,6 +1019,35 @@ void bottom64_rerun(apm_ctx* c, int count, const std::vector<int>& redo) {
     c->n_post64 += (int64_t)redo.size();
 }
 
+// The reference's own route to chol(C) (estimators.py:206-215, lpa.py:107-112) for the chains
+// whose C is small against K (bit 3 of Sl.chain_wide, APM_ICM_Q): C = K - V^T V with
+// V = L^-1 W^1/2 K and L = chol(B) of the last Newton iteration, all fp64, as the bottom-right
+// block of the factorisation of the augmented matrix [[B, .], [K W^1/2, K]] (k_form_B +
+// k_form_aug, then one blocked Cholesky of 2N columns). The push-through factor the estimate uses
+// cannot fail (M is SPD for any W >= 0); the reference's explicitly formed C can be numerically
+// indefinite (a property of the route: it fails under 1-ulp perturbations of B at the golden ICM
+// thetas and passes under them at configs[2]'s sigma = e^18.5, tools/icm_route_study.py). A chain
+// whose C fails here gets APM_STATUS_CHOL_C, raised as InvalidCovarianceMatrixError (masked in
+// batched calls) as the reference does. Only flagged chains pay (8N^3/3 flops each); A is free
+// by now. (At the golden ICM thetas the device's chol(K) fails first: K's definiteness there is
+// below its rounding)
+void icm_check(apm_ctx* c, int count, const std::vector<int>& chk) {
+    const int nb = c->nb;
+    for (int b = 0; b < count; ++b) c->hmask[b] = 0;
+    for (int b : chk) c->hmask[b] = 1;
+    HIPC(hipMemcpyAsync(c->active2, c->hmask, sizeof(int) * count, hipMemcpyHostToDevice,
+                        c->stream));
+    const Live lr{c->active2, c->status};
+    launch_form_B(c->K, c->A, c->v, c->np, lr, count, c->stream);
+    check_launch();
+    launch_form_aug(c->K, c->A, c->v, c->np, lr, count, c->stream, !c->k_full);
+    check_launch();
+    const Exec ex{c->stream, lr, c->Dinv, c->ldet, (int)chk.size()};
+    chol_range(c, c->A, 0, 2 * nb, 2 * nb, 2 * nb, APM_STATUS_CHOL_C, count, true, 0, no_gap,
+               &ex);
+    c->n_icm_check += (int64_t)chk.size();
+}
+
 // fp64 factor buffers of wide slots (Sl.L64): attached on demand, recycled through l64_free
 void attach_l64(apm_ctx* c, int64_t slot) {
     if (c->l64_h[slot]) return;
@@ -1175,6 +1219,9 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                       RB{c->n_iter, (int)sizeof(int) * count, it_h.data()},
                       RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
         const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
+        std::vector<int> chk;  // bit 3: the reference's route to chol(C) is checked (icm_check)
+        for (int b = 0; b < count; ++b)
+            if (st_h[b] == 0 && (wide_h[b] & 8) && est == APM_EST_IS && c->icm) chk.push_back(b);
         std::vector<int> redo, rewrite;  // fp32 bottom blocks above the trace bound (bit 1);
         bool attached = false;           // wide slots whose fp64 factor was not written (bit 2)
         for (int b = 0; b < count; ++b) {
@@ -1204,6 +1251,10 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
             read_back(c, {RB{c->out, (int)sizeof(double) * count, out_logf},
                           RB{c->status, (int)sizeof(int) * count, st_h.data()},
                           RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
+        }
+        if (!chk.empty()) {  // (after everything that reads A)
+            icm_check(c, count, chk);
+            read_back(c, {RB{c->status, (int)sizeof(int) * count, st_h.data()}});
         }
         bool detached = false;
         for (int b = 0; b < count; ++b) {
@@ -1254,6 +1305,8 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_Q256")) c->q256 = atoi(e) != 0;
     if (const char* e = getenv("APM_DFINV")) c->dfinv = atoi(e) != 0;
     if (const char* e = getenv("APM_SYMV_TPW")) c->symv_tpw = atoi(e);
+    if (const char* e = getenv("APM_ICM")) c->icm = atoi(e) != 0;
+    if (const char* e = getenv("APM_ICM_Q")) c->icm_q = std::max(1.0, atof(e));
     // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
     // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
@@ -1323,7 +1376,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 24, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 32, hipHostMallocDefault));
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hmask), sizeof(int) * (size_t)B,
                        hipHostMallocDefault));
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 20,
@@ -1331,6 +1384,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
     c->h3ok = dalloc<int>(c, 2 * B);
     c->h3post = c->h3ok + B;
+    c->icm_thr = dalloc<double>(c, B);
     // + 3: the bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS) and of the
     // TRSV (APM_PROF_TRSV_TIMEOUTS), the arrival-ticket counter (spin_words)
     if (c->mixed && c->df32 && c->h3 && c->planes_on) {
@@ -1367,6 +1421,7 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     if (const char* e = getenv("APM_WIDE_Q")) c->Sl.wide_q = atof(e);  // development knob
     if (const char* e = getenv("APM_POST32_Q")) c->Sl.post_q = atof(e);
     c->Sl.post_q = std::min(c->Sl.post_q, c->Sl.wide_q);  // (a wide slot needs the fp64 factor)
+    c->Sl.icm_thr = c->icm_thr;
     HIPC(hipMemset(c->Sl.cst, 0, sizeof(double) * n_slots));
     HIPC(hipMemset(c->Sl.wide, 0, sizeof(int) * n_slots));
     c->slot_wide.assign((size_t)n_slots, 0);
@@ -1567,6 +1622,7 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
         for (int64_t b = 0; b < count; ++b) {
             pin_h3(c)[b] = c->h3 && th[b * c->P] < 19.0;
             pin_h3post(c)[b] = c->h3 && 1.0 + c->n * (std::exp(th[b * c->P]) + c->eps) < 4e8;
+            pin_icm(c)[b] = c->n * (std::exp(th[b * c->P]) + c->eps) / c->icm_q;  // K_ii
         }
         upload_h3(c, (int)count);
         if (est != APM_EST_LAPLACE) upload_idx(c, (int)count, slots, ubufs);
@@ -1599,6 +1655,7 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
         pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
         pin_h3post(c)[0] = c->h3 && 1.0 + c->n * kmax < 4e8;
+        pin_icm(c)[0] = c->n * kmax / c->icm_q;
         upload_h3(c, 1);
         upload_idx(c, 1, &slot, &ubuf);  // (the pinned copy is the slot the read-back marks)
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);

@@ -189,8 +189,10 @@ void launch_copy_lower(MatB src, MatB dst, int np, Live live, int nchains, hipSt
 //    [ K W^1/2    K  ]   ---------->      [ V^T    C_chol ]      V = L^-1 W^1/2 K,
 //    [ 0      f_post^T]]                  [ 0      g^T    ]]     C = K - V^T V, g = C_chol^-1 f_post
 // The top-left (L of the last Newton iteration) is already factored; this fills rows [np, 2np+64).
+// lower_only: K holds its lower tiles only (the theta-call's Gram); the upper block of K W^1/2
+// then reads K's symmetric entry
 __global__ __launch_bounds__(256) void k_form_aug(MatB K, MatB A, NewtonVecs v, int nb,
-                                                  Live live) {
+                                                  Live live, int lower_only) {
     const int b = blockIdx.y;
     if (!live_b(live, b)) return;
     const int t = blockIdx.x;
@@ -204,7 +206,9 @@ __global__ __launch_bounds__(256) void k_form_aug(MatB K, MatB A, NewtonVecs v, 
         const int ti = t / nb, tj = t % nb;
         for (int e = tid; e < 4096; e += 256) {
             const int r = ti * 64 + (e >> 6), c = tj * 64 + (e & 63);
-            Ab[(np + r) * A.ld + c] = Kb[(int64_t)r * K.ld + c] * Ws[c];
+            const double kv = (lower_only && c > r) ? Kb[(int64_t)c * K.ld + r]
+                                                    : Kb[(int64_t)r * K.ld + c];
+            Ab[(np + r) * A.ld + c] = kv * Ws[c];
         }
     } else if (t < nbl + ntri) {  // bottom-right lower tiles: K
         int ti, tj;
@@ -224,10 +228,10 @@ __global__ __launch_bounds__(256) void k_form_aug(MatB K, MatB A, NewtonVecs v, 
 }
 
 void launch_form_aug(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains,
-                     hipStream_t s) {
+                     hipStream_t s, bool lower_only) {
     const int nb = np / 64;
     hipLaunchKernelGGL(k_form_aug, dim3(nb * nb + nb * (nb + 1) / 2 + 2 * nb, nchains), dim3(256),
-                       0, s, K, A, v, nb, live);
+                       0, s, K, A, v, nb, live, (int)lower_only);
 }
 
 // Laplace LML (latent_posterior_approximations.py:103-106), with -sum log L_ii = -sum_k ldet[k]
@@ -370,7 +374,9 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
         // attaches an fp64 buffer to the slot of every chain with bit 2)
         const int wd = tq > S.wide_q && mode != 3 ? 1 : 0;
         S.wide[slots[b]] = wd;
-        S.chain_wide[b] = wd | (mode == 3 && tq > S.post_q ? 2 : 0) | (tq > S.wide_q ? 4 : 0);
+        // bit 3: C's mean diagonal below 1e-3 of K's (cancellation in the reference's K - V^T V)
+        S.chain_wide[b] = wd | (mode == 3 && tq > S.post_q ? 2 : 0) | (tq > S.wide_q ? 4 : 0) |
+                          (S.icm_thr && mode != 1 && tq < S.icm_thr[b] ? 8 : 0);
         double c = 0.0;
         if (mode != 1) {
             double ld = 0.0;

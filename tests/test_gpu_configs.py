@@ -195,6 +195,25 @@ def test_config2_stationary_states_match_fp64_newton(nat, monkeypatch):
         assert np.abs(f[b] - ref[4][b]).max() <= FPOST_REL * np.abs(ref[4][b]).max(), b
 
 
+def test_config2_reference_route_check_passes_everywhere(nat, monkeypatch):
+    """The reference-route check of chol(C) (capi.cpp icm_check) forced on
+    every chain (APM_ICM_Q huge) at configs[2]'s four thetas, sigma = e^18.5 included: C =
+    K - V^T V of the last Newton iteration factors on every chain (status 0, as in the
+    reference, which returned values there) and the estimates are bitwise those of the default
+    call (the check writes nothing the estimate reads)."""
+    from gpdemo.utils import synthetic_gp_data
+    z = golden('config2_ref')
+    X, y = synthetic_gp_data(int(z['n']), int(z['d']), int(z['data_seed']))
+    th = z['thetas'].astype(np.float64)
+    U = np.random.RandomState(int(z['u_seed'])).normal(size=(int(z['n']), int(z['s'])))
+    ref = _run(nat, X, y, th, int(z['s']), U, monkeypatch)
+    o, st, nops, o2, f = _run(nat, X, y, th, int(z['s']), U, monkeypatch, APM_ICM_Q='1e300')
+    assert (ref[1] == 0).all() and (st == 0).all()
+    np.testing.assert_array_equal(o, ref[0])
+    np.testing.assert_array_equal(o2, ref[3])
+    np.testing.assert_array_equal(nops, ref[2])
+
+
 def test_config0_pmmh_chain_matches_reference(nat):
     import auxpm.samplers as smp
     import gpdemo.estimators as est

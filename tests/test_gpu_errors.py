@@ -100,24 +100,85 @@ def test_failing_chain_masked_in_batch(nat):
     ctx.close()
 
 
+def _k_indefinite_under_rounding(K, rel=1e-15, draws=10):
+    """LAPACK's chol(K) fails on every draw of K * (1 + rel * noise) (symmetrised): K's
+    definiteness is decided below the Gram's stated accuracy (2e-15 x |log K|)."""
+    import scipy.linalg as la
+    rng = np.random.RandomState(0)
+    for _ in range(draws):
+        Kp = K * (1 + rel * rng.standard_normal(K.shape))
+        try:
+            la.cholesky((Kp + Kp.T) / 2, lower=True)
+            return False
+        except la.LinAlgError:
+            pass
+    return True
+
+
 @pytest.mark.parametrize('name', ['icm_a', 'icm_b'])
-def test_invalid_covariance_deviation_pinned(nat, name):
-    """At both thetas where the reference raises InvalidCovarianceMatrixError, K itself is
-    numerically singular: its smallest eigenvalue is below n eps lambda_max (the 1e-8 jitter is
-    ~14 ulp of sigma^2 = e^15 .. e^16), so the sign of chol(K)'s trailing pivots is rounding
-    noise. LAPACK's chol(K) happened to pass there and chol(C) failed. The device either fails
-    chol(K) the same way (-> LinAlgError, as estimators.py:206 would) or passes it and returns
-    the push-through estimate, which is then pinned to the oracle's fp64 statement of that route.
-    Either way the chain's behaviour is a failure / an estimate the reference's op order cannot
-    produce reliably; no ICM search found a theta with a well-conditioned K."""
+def test_invalid_covariance_raises_where_the_reference_raises(nat, name):
+    """At both thetas where the reference raises InvalidCovarianceMatrixError
+    (estimators.py:208-215; tests/golden/errors.npz) the device raises too, never returning an
+    estimate. The estimate's push-through factor cannot fail (M is SPD for any W >= 0), so for
+    chains whose C is small against K (APM_ICM_Q) the library also forms C the reference's way
+    (C = K - V^T V from the last Newton iteration's fp64 B factor, the augmented-matrix route,
+    capi.cpp icm_check) and fails the chain with APM_STATUS_CHOL_C when its Cholesky does; that
+    failure is a property of the route (it fails under 1-ulp perturbations of B as well,
+    profiles/r05_icm_route_study.txt), while at configs[2]'s sigma = e^18.5 the same route passes
+    (test_config2_full_size_vs_reference keeps that chain's value). Where the device's chol(K)
+    fails first (LinAlgError, estimators.py:206) K's own definiteness is rounding noise: LAPACK's
+    chol(K) fails on every 1e-15-relative perturbation of the reference's K there."""
     e = golden('errors')
     assert str(e[name + '_raised']) == 'InvalidCovarianceMatrixError'
     X, y, ns = e['extreme_X'], e['extreme_y'], e['extreme_ns']
     th = e[name + '_theta']
+    es = est.LogMarginalLikelihoodApproxPosteriorISEstimator(
+        X, y, krn.make_kernel_func('iso', 1e-8), lpa.laplace_approximation)
+    with pytest.raises((est.InvalidCovarianceMatrixError, np.linalg.LinAlgError)) as ei:
+        es(ns, th)
+    print(name, type(ei.value).__name__, ei.value)
+    if not isinstance(ei.value, est.InvalidCovarianceMatrixError):
+        assert 'Cholesky of K' in str(ei.value)
+        K = np.empty((X.shape[0],) * 2)
+        orc.make_kernel_func('iso', 1e-8)(K, X, th)
+        assert _k_indefinite_under_rounding(K)
+
+
+@pytest.mark.parametrize('name', ['icm_a', 'icm_b'])
+def test_invalid_covariance_from_the_references_K(nat, name):
+    """The same thetas with the reference's own K uploaded (its Cython Gram's output,
+    tests/golden/icm_k.npz from make_golden_icm.py; any kernel callable other than
+    make_kernel_func's takes the host-K path, apm_theta_eval_K): on that exact K the reference's
+    chol(K) passes and its chol(C) fails. The device raises InvalidCovarianceMatrixError through
+    the reference-route check (capi.cpp icm_check) when its own chol(K) passes there too, and
+    LinAlgError where its blocked chol(K) rounds K to indefinite (see above)."""
+    e = golden('errors')
+    Kref = golden('icm_k')[name + '_K']
+    X, y, ns = e['extreme_X'], e['extreme_y'], e['extreme_ns']
+
+    def ref_k(K, X_, theta):
+        K[...] = Kref
+
+    es = est.LogMarginalLikelihoodApproxPosteriorISEstimator(X, y, ref_k,
+                                                             lpa.laplace_approximation)
+    with pytest.raises((est.InvalidCovarianceMatrixError, np.linalg.LinAlgError)) as ei:
+        es(ns, e[name + '_theta'])
+    print(name, 'reference K:', type(ei.value).__name__, ei.value)
+    if not isinstance(ei.value, est.InvalidCovarianceMatrixError):
+        assert 'Cholesky of K' in str(ei.value)
+        assert _k_indefinite_under_rounding(Kref)
+
+
+@pytest.mark.parametrize('name', ['icm_a', 'icm_b'])
+def test_invalid_covariance_check_off_is_pushthrough(nat, monkeypatch, name):
+    """APM_ICM=0 (no reference-route check): the device either fails chol(K) as above or returns
+    the push-through estimate, pinned to the oracle's fp64 statement of that route (round 4)."""
+    e = golden('errors')
+    X, y, ns = e['extreme_X'], e['extreme_y'], e['extreme_ns']
+    th = e[name + '_theta']
     K = np.empty((X.shape[0],) * 2)
     orc.make_kernel_func('iso', 1e-8)(K, X, th)
-    w = np.linalg.eigvalsh(K)
-    assert w[0] < K.shape[0] * np.finfo(float).eps * w[-1]
+    monkeypatch.setenv('APM_ICM', '0')
     es = est.LogMarginalLikelihoodApproxPosteriorISEstimator(
         X, y, krn.make_kernel_func('iso', 1e-8), lpa.laplace_approximation)
     try:
