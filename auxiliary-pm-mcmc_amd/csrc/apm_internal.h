@@ -106,17 +106,21 @@ struct Planes16 {
 // dataflow launch (chol32.hip: per-(chain, row) progress words prog[b * pstride + row], monotonic
 // base per factorisation and panel); returns the launch's workgroup count (its tickets), 0 when
 // nothing was launched, -1 for a panel wider than the progress word allows. pl.base != nullptr:
-// the rows below the diagonal block (row tiles < pl.rows / 64) also write the panel's planes
+// the rows below the diagonal block (row tiles < pl.rows / 64) also write the panel's planes.
+// inv_skip (per chain): that chain's rows below the diagonal block return at once (its
+// explicit-inverse panel follows)
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
                             Planes16 pl = Planes16{nullptr, 0, 0, 0}, int rhs_as = -1,
-                            bool inv_skip = false);
+                            const int* inv_skip = nullptr);
 // explicit-inverse panel of the Newton factorisation (chol32.hip), after a dataflow launch over
 // the diagonal block [K, K+8) and the right-hand-side row (rhs_as): Z = inv(L_D) of the 512x512
 // diagonal block as fp16x3 planes (zpl, 512 rows), by recursive doubling over fp32 scratch (zt:
 // 3 x 512 x 512 per chain, zstride floats apart); then every row tile i in [K+8, nb) becomes
-// X_i = A_i Z^T in one fp16x3 GEMM (in place, plus the panel's planes pl). Chains with h3ok only.
+// X_i = A_i Z^T in one fp16x3 GEMM (in place, plus the panel's planes pl). Only the chains
+// flagged in `ok` (the host's invok: 1 + K_ii < 2^15, so the split Schur-complement entries fit
+// fp16's range).
 void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstride, float* zt,
                         int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
                         const int* h3ok, hipStream_t s);
@@ -255,7 +259,8 @@ struct SlotSet {
 // Only chains with live.active[b] && !live.status[b] are written.
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
-                       int nchains, hipStream_t s, MatF S32 = MatF{nullptr, 0, 0});
+                       int nchains, hipStream_t s, MatF S32 = MatF{nullptr, 0, 0},
+                       double* rowe = nullptr);
 // the fp64 factor alone, for the call's wide slots that have a buffer attached (mode 1 or 2)
 void launch_slot_write_L64(MatB A, SlotSet S, const int64_t* slots, int mode, int np, Live live,
                            int nchains, hipStream_t s);
@@ -318,3 +323,32 @@ void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs
 void launch_lme(const double* partial, int64_t pstride, int nb, int S, int sp, SlotSet Sl,
                 const int64_t* slots, double* out, const int* status, int nchains,
                 hipStream_t s);
+
+// chol(K) retry of the chains with fail[b] == code, unblocked in LAPACK's dpotf2 order (chol.hip,
+// DESIGN.md §3.4): K's lower triangle into A, L in place, per-tile log-diagonal sums into ldet;
+// success clears fail[b]. Returns false (nothing launched) for np > 512.
+bool launch_chol_unblocked(MatB K, MatB A, int np, int* fail, int code, double* ldet,
+                           int64_t lstride, int nchains, hipStream_t s);
+
+// ---- the guard (newton.hip) --------------------------------------------------
+// G[k * B + b]: 0: 1/2 log|B| of the last Newton factor, 1: 1/2 log|K|, 2..5: residuals r1..r4
+// (rowe: the slot writer's per-row residuals of C_chol g = f_post, B x np)
+void launch_guard_save(const double* ldet, int64_t lstride, int off, int nb, double* G, int B,
+                       int k, Live live, int nchains, hipStream_t s);
+void launch_guard_check(const double* ldet, int64_t lstride, int nb, const double* gvec,
+                        int64_t gstride, SlotSet S, const int64_t* slots, double* G, int B,
+                        double t1, double t2, double t3, double t4, const double* rowe,
+                        const double* fvec, int fail_code, Live live, int nchains,
+                        hipStream_t s);
+
+// ---- stream skew (tests only; capi.cpp skew_point, APM_SKEW) ------------------------------
+// Every launch goes through APM_LAUNCH, which first lets skew_point enqueue a delay kernel on the
+// launch's stream when the calling thread's context asked for it: a cross-stream edge without
+// its wait then reads stale data deterministically instead of by chance.
+void skew_point(hipStream_t s);
+void launch_delay(int us, hipStream_t s);
+#define APM_LAUNCH(kern, grid, block, lds, st, ...)                      \
+    do {                                                                 \
+        skew_point(st);                                                  \
+        hipLaunchKernelGGL(kern, grid, block, lds, st, __VA_ARGS__);     \
+    } while (0)

@@ -36,15 +36,47 @@ struct ProfRec {
 // ~log10(APM_ICM_Q) digits or more (1e-7 of K_ii at the golden ICM theta icm_a, 1e-5 at icm_b;
 // ~1/4 at configs[2]'s sigma = e^18.5, and no chain of the bench's stationary states: unchecked)
 #define APM_ICM_Q 1.0e3
+// the guard's bounds (k_guard_check): r1 nats of 1/2 log-determinant between the
+// last Newton factor (fp32 with fp16x3 updates) and the fp64 posterior factor, r2 relative, r3
+// nats between the fp32 slot's log-diagonal and the fp64 log-determinants, r4 max |C_chol g -
+// f_post| over the rows relative to max(1, max |f_post|); measured maxima in
+// DESIGN.md §11 (tests/test_gpu_errors.py::test_guard_residuals_are_rounding_sized)
+#define GUARD_T1 1.0
+#define GUARD_T2 1.0e-6
+#define GUARD_T3 5.0e-2
+#define GUARD_T4 1.0e-4
+
+// The cross-stream edges of a theta-call, one event each (DESIGN.md §11 names the producer and
+// the consumer of every one). No event is recorded again before the wait that names its previous
+// record has been enqueued: the per-panel edges are indexed by panel; the Newton lookahead's
+// per-panel pair is recorded once per factorisation, and a factorisation starts only after the
+// previous one's last far update was joined into the main stream.
+struct Edges {
+    hipEvent_t gram_k = nullptr;       // main -> s2: the Gram wrote K (and BL's first panel)
+    hipEvent_t cholk_done = nullptr;   // s2 -> main: L_K final in BL, its log-det in ldet + nb
+    hipEvent_t y2 = nullptr;           // main -> s2: L_K J formed in BL (k_form_y2_rev)
+    hipEvent_t bottom_done = nullptr;  // s2 -> main: the fp32 bottom block (S32) final
+    std::vector<hipEvent_t> cholk_rel; // main -> s2, per chol(K) panel: its release (no data)
+    std::vector<hipEvent_t> lp_panel;  // main -> s2, per panel of L': tiles and inverses final
+    std::vector<hipEvent_t> df;        // main -> s3, per Newton panel: its columns + planes final
+    std::vector<hipEvent_t> far;       // s3 -> main, per Newton panel: its far update done
+    std::vector<hipEvent_t*> all() {
+        std::vector<hipEvent_t*> v{&gram_k, &cholk_done, &y2, &bottom_done};
+        for (auto* w : {&cholk_rel, &lp_panel, &df, &far})
+            for (hipEvent_t& e : *w) v.push_back(&e);
+        return v;
+    }
+};
+
 struct apm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int kind = 0, n = 0, d = 0, np = 0, nb = 0, P = 0, S = 0, sp = 0;
     int max_batch = 0, n_slots = 0, n_ubufs = 0;
-    // tiles per outer panel of the fp64 factorisations (APM_OUTER) and of the Newton matrix
-    // (<= 14: the dataflow panel's progress word packs the column step in 4 bits, 15 = failed;
-    // rhs_row_update32 covers a depth of 16 tiles)
-    int outer = 8, outer32 = 8;
+    // tiles per outer panel of the fp64 factorisations and of the Newton matrix (<= 14: the
+    // dataflow panel's progress word packs the column step in 4 bits, 15 = failed;
+    // rhs_row_update32 covers a depth of 16 tiles; the explicit-inverse panels need 8)
+    static constexpr int outer = 8, outer32 = 8;
     std::vector<int> slot_refs;  // owners of each cache slot (apm_cache_*; 0 = free)
     std::vector<int> slot_wide;  // host mirror of Sl.wide (read back with each theta-call)
     // fp64 factors of the wide slots: one np x np buffer attached per wide slot (Sl.L64 is the
@@ -72,9 +104,9 @@ struct apm_ctx {
     double* refine_prev = nullptr;  // max|d| of the previous refinement step per chain
     int64_t n_refine_steps = 0, n_fp64_rerun = 0;  // statistics (apm_prof_read APM_PROF_STATS)
     int64_t n_icm_check = 0;  // chains whose C was formed the reference's way (icm_check)
-    // APM_ICM=0: no check of the reference's chol(C) (icm_check); APM_ICM_Q: its threshold
-    // (development knob: a huge value checks every chain)
-    bool icm = true;
+    int64_t n_guard = 0;      // chains failed by the guard (APM_STATUS_GUARD)
+    // APM_ICM_Q: the threshold of the check of the reference's chol(C) (icm_check; test knob: a
+    // huge value checks every chain, 0 checks none)
     double icm_q = APM_ICM_Q;
     int64_t *d_slots = nullptr, *d_ubufs = nullptr, *d_i3 = nullptr;  // d_ubufs = d_slots + B
     // pinned host staging of the per-call uploads (one H2D of slots + ubufs; the per-chain
@@ -110,33 +142,28 @@ struct apm_ctx {
     bool h3 = true;       // APM_H3=0: fp32 operands in the fp32 factorisations' outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
     bool h3_all = false;  // ... and every chain may (the quad-tile far updates need that)
-    // far trailing updates of the Newton factorisation on 256x256 quad tiles (k_chol_update32_q256,
-    // needs the planes; APM_Q256=0: the 128-row super-tile kernel)
-    bool q256 = true;
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
     int* h3post = nullptr;  // the same for the posterior factor's fp32 bottom block (h3ok + B)
+    // per chain: explicit-inverse Newton panels allowed (h3ok + 2B): their fp16x3 operands are
+    // Schur-complement entries of B, bounded by max B_ii <= 1 + K_ii (not by sqrt(B_ii) as the
+    // walk's solved entries are), so the range check is on 1 + K_ii itself (chol32.hip)
+    int* invok = nullptr;
+    bool inv_any = false, inv_all = false;
     double* icm_thr = nullptr;  // per chain: SlotSet::icm_thr
     // the bottom block of the posterior factor [[J M J],[L_K J]] (the TRSM that yields chol(C) J)
-    // in fp32 after the fp64 factorisation of J M J (postcov.hip; APM_POST32=0: all fp64); chains
-    // whose trace(C) exceeds Sl.post_q are recomputed in fp64 (n_post64 counts them)
-    int post32 = 2;  // 1: after the fp64 factorisation of J M J; 2: panel by panel beside it
+    // in fp32 panel by panel beside the fp64 factorisation of J M J (postcov.hip); chains whose
+    // trace(C) exceeds Sl.post_q are recomputed in fp64 (n_post64 counts them)
     int* hmask = nullptr;  // pinned: the chains of such a recomputation
     int64_t n_post64 = 0;
-    // in-panel factorisation of the Newton matrix: one dataflow launch per outer panel
-    // (k_chol_panel_df32; APM_DF32=0: the launch sequence it replaces)
-    bool df32 = true;
-    // the dataflow launch also writes the panel's fp16x3 operand planes (Planes16), which the
-    // trailing update stages with LDS-DMA instead of splitting fp32 operands in registers (two
-    // buffers by panel parity: the lookahead's far update reads panel K's while the dataflow
-    // launch of K + 1 writes its own; APM_PLANES=0: split while staged)
-    bool planes_on = true;
+    // the Newton factorisation's dataflow launches also write the panel's fp16x3 operand planes
+    // (Planes16), which the trailing updates stage with LDS-DMA (two buffers by panel parity: the
+    // lookahead's far update reads panel K's while the dataflow launch of K + 1 writes its own)
     unsigned short* planes = nullptr;
     int64_t plane_cs = 0;  // halves per chain and buffer
-    // explicit-inverse panels (APM_DFINV, chol32.hip k_zinv_* / k_panel_inv_gemm32): the
-    // dataflow launch walks the diagonal block and the right-hand-side row only; Z = inv(L_D) per
-    // chain (fp32 scratch zt: Z, Z^T, T^T; fp16x3 planes zplanes) and one GEMM per row tile below
-    bool dfinv = true;
-    int symv_tpw = 2;  // K x: lower tiles per workgroup (APM_SYMV_TPW: 1, 2 or 4)
+    // explicit-inverse panels (chol32.hip k_zinv_* / k_panel_inv_gemm32): the dataflow launch
+    // walks the diagonal block and the right-hand-side row only; Z = inv(L_D) per chain (fp32
+    // scratch zt: Z, Z^T, T^T; fp16x3 planes zplanes) and one GEMM per row tile below
+    static constexpr int symv_tpw = 2;  // K x: lower tiles per workgroup
     float* zt = nullptr;
     unsigned short* zplanes = nullptr;
     // per (chain, row tile) progress words, then [dataflow timeouts][TRSV timeouts][ticket]
@@ -149,19 +176,19 @@ struct apm_ctx {
     // chains whose work the roofline accounting credits (Newton: the unconverged ones after the
     // previous convergence read; update_flops x live_n instead of x count)
     int live_n = 0;
-    // chol(K) of the IS theta-call on a low-priority second stream, concurrent with the Newton
-    // iterations (APM_OVERLAP_K=0: after them, on the main stream)
-    bool overlap_k = true;
+    // chol(K) of the mixed-precision IS theta-call on a low-priority second stream, concurrent
+    // with the Newton iterations, and the fp32 bottom block of the posterior factor on the same
+    // stream; the far part of each Newton trailing update on stream3 beside the next panel's
+    // dataflow launch (one-panel lookahead, chol_range32)
     hipStream_t stream2 = nullptr;
-    // one-panel lookahead of the Newton factorisation (APM_LOOKAHEAD, chol_range32): the far part
-    // of each trailing update on stream3 beside the next panel's dataflow launch
-    bool lookahead = true;
     hipStream_t stream3 = nullptr;
-    hipEvent_t ev_la[4] = {nullptr, nullptr, nullptr, nullptr};
-    int la_i = 0;
-    hipEvent_t ev_gram = nullptr, ev_cholk = nullptr;
-    hipEvent_t ev_feed[4] = {nullptr, nullptr, nullptr, nullptr};
-    int feed_i = 0;
+    Edges ev;  // one event per cross-stream edge
+    int skew = 0;  // APM_SKEW (tests only): delay kernels in front of launches (skew_point), bit 2
+                   // drops the bottom_done wait
+    // per-chain guard data (k_guard_*): [1/2 log|B| of the last Newton factor][1/2 log|K|]
+    // [residuals r1 .. r4 of the last theta-call]
+    double* guard = nullptr;
+    double* guard_rows = nullptr;  // the slot writer's row residuals of C_chol g = f_post (B x np)
     int *active2 = nullptr, *status2 = nullptr;
     // chol(K) is enqueued one outer panel at a time, each released when the main stream enters a
     // single-workgroup-per-chain TRSV (3/4 of the CUs idle) - see feed_chol_k
@@ -170,6 +197,36 @@ struct apm_ctx {
     // first trailing update then reads its old tiles from K (out of place, k_chol_update_t128 S)
     bool cholk_partial = false;
 };
+
+// ------------------------------------------------------------------------------- APM_SKEW
+// (tests only) the calling thread's context selects delay kernels in front of every launch on
+// its secondary streams (bit 0: chol(K), the posterior's bottom block, the Newton far updates)
+// and/or its main stream (bit 1). Every cross-stream edge is an event (Edges); with one side of
+// an edge held back by the delays, a missing or misplaced wait shows as a changed result, which
+// tests/test_gpu_errors.py::test_stream_skew_is_bitwise_neutral compares bitwise.
+namespace {
+struct SkewState {
+    int mode = 0;
+    hipStream_t main = nullptr, s2 = nullptr, s3 = nullptr;
+};
+thread_local SkewState t_skew;
+constexpr int SKEW_US_SECONDARY = 1000, SKEW_US_MAIN = 40;
+struct SkewScope {  // an API entry point's launches belong to context c
+    SkewState prev;
+    explicit SkewScope(const apm_ctx* c) : prev(t_skew) {
+        t_skew = SkewState{c->skew & 3, c->stream, c->stream2, c->stream3};
+    }
+    ~SkewScope() { t_skew = prev; }
+};
+}  // namespace
+
+void skew_point(hipStream_t s) {
+    if (!t_skew.mode || !s) return;
+    if ((t_skew.mode & 1) && (s == t_skew.s2 || s == t_skew.s3))
+        launch_delay(SKEW_US_SECONDARY, s);
+    else if ((t_skew.mode & 2) && s == t_skew.main)
+        launch_delay(SKEW_US_MAIN, s);
+}
 
 namespace {
 
@@ -486,7 +543,7 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     // outside the profiled scope: the roofline's launches are the quad and 128-row GEMMs)
     const int rhs = R > c->nb || jext > 0 ? c->nb : -1;
     const bool quad =
-        outer && pl.base && fuse_k < 0 && c->q256 && c->h3_all && i0 < c->nb && jext <= 0;
+        outer && pl.base && fuse_k < 0 && c->h3_all && i0 < c->nb && jext <= 0;
     {
         const int Rg = quad ? std::min(R, c->nb) : R;
         const double fl = c->prof ? update_flops(i0, Rg, j0, jend, kc, Gap{0, 0}) * c->live_n : 0.0;
@@ -516,94 +573,75 @@ void tracked_update32(apm_ctx* c, MatF M, int k0, int kc, int i0, int R, int j0,
     }
 }
 
-// chol_range's twin for the fp32 Newton matrix (same steps, same fused diag)
+// chol_range's twin for the fp32 Newton matrix: one dataflow launch per outer panel
+// (k_chol_panel_df32: the in-panel steps, fused diagonal tiles), the explicit-inverse panel for
+// the chains invok allows, and the trailing update with a one-panel lookahead (the far part on
+// stream3 beside the next panel's dataflow launch)
 void chol_range32(apm_ctx* c, MatF M, int k0, int k1, int R, int Cb, int fail_code, int count) {
     const Live lv = live_of(c);
     float* D = dinv32_of(c);
     const int64_t ds = 2 * c->dstride;
     bool have_diag = false;
     const unsigned long long fact = ++c->df_fact;
-    bool far_pending = false;  // a far update on stream3 not yet joined (lookahead)
-    hipEvent_t e_far = nullptr;
+    int far_pending = -1;  // the panel whose far update on stream3 is not yet joined
     for (int K = k0; K < k1; K += c->outer32) {
         const int Kend = std::min(K + c->outer32, k1);
-        if (c->df32) {  // the same steps in one dataflow launch per outer panel (chol32.hip)
-            if (!have_diag) {
-                launch_chol_diag32(M, K, D, ds, c->ldet, c->lstride, lv, fail_code, count,
-                                   c->stream);
-                check_launch();
-            }
-            // explicit-inverse panel for the fp16x3 chains; with every chain fp16x3 the dataflow
-            // launch covers the diagonal block and the right-hand-side row only, else all rows,
-            // those of the fp16x3 chains below the diagonal block returning at once
-            const bool inv = c->dfinv && c->zt && Kend - K == 8 && Kend < c->nb &&
-                             R <= c->nb + 1 && planes_of(c, K).base;
-            const bool compact = inv && c->h3_all;
-            const long tickets = launch_chol_panel_df32(
-                M, K, Kend - K, compact ? Kend + (R > c->nb ? 1 : 0) : R,
-                FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv, count,
-                c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
-                (fact << 16) | ((unsigned long long)(K / c->outer32) << 4), spin_ctl(c, false),
-                c->stream, planes_of(c, K), compact && R > c->nb ? c->nb : -1, inv && !compact);
-            if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
+        const int p = K / c->outer32;
+        if (!have_diag) {
+            launch_chol_diag32(M, K, D, ds, c->ldet, c->lstride, lv, fail_code, count, c->stream);
             check_launch();
-            c->ticket_base += (unsigned long long)tickets;
-            if (inv) {  // the rows below the diagonal block: X_i = A_i inv(L_D)^T
-                const int64_t zcs = 2 * 16 * 512 * 32;
-                launch_panel_inv32(M, K, c->nb, D, ds, c->zt, 3 * 512 * 512,
-                                   Planes16{c->zplanes, zcs, zcs / 2, 512}, planes_of(c, K), lv,
-                                   count, c->h3ok, c->stream);
-                check_launch();
-            }
-            have_diag = Kend < k1;
-            const int Knext = std::min(Kend + c->outer32, Cb);
-            if (c->lookahead && Knext < Cb) {
-                // one-panel lookahead: the next panel's columns first (narrow, with the fused
-                // diagonal tile), its dataflow launch next on this stream, and the rest of the
-                // trailing update (far: columns >= Knext) on stream3 beside it. The narrow update
-                // shares its tiles with the previous panel's far update, so it waits for that.
-                hipEvent_t e_df = c->ev_la[c->la_i++ & 3];
-                HIPC(hipEventRecord(e_df, c->stream));
-                if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
-                // (the right-hand-side row's far columns go with the narrow update on this
-                // stream: on stream3 behind the far update they held up the next narrow update)
-                tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Knext, count,
-                                 have_diag ? Kend : -1, fail_code, nullptr, planes_of(c, K),
-                                 R > c->nb ? Cb : -1);
-                HIPC(hipStreamWaitEvent(c->stream3, e_df, 0));
-                tracked_update32(c, M, K, Kend - K, Knext, std::min(R, c->nb), Knext, Cb, count,
-                                 -1, fail_code, c->stream3, planes_of(c, K));
-                e_far = c->ev_la[c->la_i++ & 3];
-                HIPC(hipEventRecord(e_far, c->stream3));
-                far_pending = true;
-                continue;
-            }
-            if (far_pending) {  // (the previous far update shares these tiles)
-                HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
-                far_pending = false;
-            }
-            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
-                             fail_code, nullptr, planes_of(c, K));
-            continue;
         }
-        // APM_DF32=0: the launch sequence the dataflow kernel replaces (left-looking inside the
-        // panel, as chol_range; bitwise the same tiles)
-        for (int k = K; k < Kend; ++k) {
-            if (k > K)
-                tracked_update32(c, M, K, k - K, k, R, k, k + 1, count, k, fail_code);
-            else if (!have_diag) {
-                launch_chol_diag32(M, k, D, ds, c->ldet, c->lstride, lv, fail_code, count,
-                                   c->stream);
-                check_launch();
-            }
-            launch_chol_panel32(M, k, k + 1, R, R, R, D, ds, lv, count, c->stream);
+        // explicit-inverse panel for the invok chains; with every chain invok the dataflow
+        // launch covers the diagonal block and the right-hand-side row only, else all rows, those
+        // of the invok chains below the diagonal block returning at once
+        const bool inv = c->inv_any && c->zt && Kend - K == 8 && Kend < c->nb &&
+                         R <= c->nb + 1 && planes_of(c, K).base;
+        const bool compact = inv && c->inv_all;
+        const long tickets = launch_chol_panel_df32(
+            M, K, Kend - K, compact ? Kend + (R > c->nb ? 1 : 0) : R,
+            FusedDiag<float>{1, D, ds, c->ldet, c->lstride, fail_code}, lv, count,
+            c->h3_now ? c->nb : 0, c->h3ok, c->dfprog, c->nb + 1,
+            (fact << 16) | ((unsigned long long)p << 4), spin_ctl(c, false), c->stream,
+            planes_of(c, K), compact && R > c->nb ? c->nb : -1, inv && !compact ? c->invok : nullptr);
+        if (tickets < 0) throw HipError{"dataflow Newton panel wider than 14 tiles"};
+        check_launch();
+        c->ticket_base += (unsigned long long)tickets;
+        if (inv) {  // the rows below the diagonal block: X_i = A_i inv(L_D)^T
+            const int64_t zcs = 2 * 16 * 512 * 32;
+            launch_panel_inv32(M, K, c->nb, D, ds, c->zt, 3 * 512 * 512,
+                               Planes16{c->zplanes, zcs, zcs / 2, 512}, planes_of(c, K), lv,
+                               count, c->invok, c->stream);
             check_launch();
         }
         have_diag = Kend < k1;
+        const int Knext = std::min(Kend + c->outer32, Cb);
+        if (Knext < Cb) {
+            // the next panel's columns first (narrow, with the fused diagonal tile), its dataflow
+            // launch next on this stream, and the rest of the trailing update (far: columns >=
+            // Knext) on stream3 beside it. Edge df[p] (main -> s3): panel p's columns, planes and
+            // the previous narrow update are final. The narrow update shares its tiles with the
+            // previous panel's far update: edge far[p-1] (s3 -> main) orders it behind that.
+            HIPC(hipEventRecord(c->ev.df[p], c->stream));
+            if (far_pending >= 0) HIPC(hipStreamWaitEvent(c->stream, c->ev.far[far_pending], 0));
+            // (the right-hand-side row's far columns go with the narrow update on this stream)
+            tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Knext, count,
+                             have_diag ? Kend : -1, fail_code, nullptr, planes_of(c, K),
+                             R > c->nb ? Cb : -1);
+            HIPC(hipStreamWaitEvent(c->stream3, c->ev.df[p], 0));
+            tracked_update32(c, M, K, Kend - K, Knext, std::min(R, c->nb), Knext, Cb, count, -1,
+                             fail_code, c->stream3, planes_of(c, K));
+            HIPC(hipEventRecord(c->ev.far[p], c->stream3));
+            far_pending = p;
+            continue;
+        }
+        if (far_pending >= 0) {  // (the previous far update shares these tiles)
+            HIPC(hipStreamWaitEvent(c->stream, c->ev.far[far_pending], 0));
+            far_pending = -1;
+        }
         tracked_update32(c, M, K, Kend - K, Kend, R, Kend, Cb, count, have_diag ? Kend : -1,
-                         fail_code);
+                         fail_code, nullptr, planes_of(c, K));
     }
-    if (far_pending) HIPC(hipStreamWaitEvent(c->stream, e_far, 0));
+    if (far_pending >= 0) HIPC(hipStreamWaitEvent(c->stream, c->ev.far[far_pending], 0));
 }
 
 void sync(apm_ctx* c) { HIPC(hipStreamSynchronize(c->stream)); }
@@ -648,25 +686,36 @@ void upload_idx(apm_ctx* c, int count, const int64_t* slots, const int64_t* ubuf
         HIPC(hipMemcpyAsync(c->d_slots, h, sizeof(int64_t) * count, hipMemcpyHostToDevice,
                             c->stream));
 }
+// pinned staging of a call's per-chain flags, [16B, 28B) of hpin: fp16x3 allowed (h3ok), for
+// the posterior bottom block (h3post), explicit-inverse panels (invok) - the layout of the
+// device block h3ok .. h3ok + 3B, uploaded with one copy - then the icm thresholds [32B, 40B)
 int* pin_h3(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 16 * c->max_batch); }
 int* pin_h3post(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 20 * c->max_batch); }
-double* pin_icm(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 24 * c->max_batch); }
+int* pin_inv(apm_ctx* c) { return reinterpret_cast<int*>(c->hpin + 24 * c->max_batch); }
+double* pin_icm(apm_ctx* c) { return reinterpret_cast<double*>(c->hpin + 32 * c->max_batch); }
 
-// per-chain fp16x3 flags of a theta-call -> device (chol32.hip: |L_ij| <= sqrt(1 + K_ii) must
-// stay below fp16's range); h3_now = any chain flagged (else the fp32-operand kernel launches)
+// per-chain range flags of a theta-call -> device. fp16x3 operands (chol32.hip): the walk's and
+// the trailing updates' operands are solved entries of L, |L_ij| <= sqrt(B_ii) <= sqrt(1 + K_ii)
+// (probit W < 1); the explicit-inverse panel also splits Schur-complement entries of B itself,
+// |A_ij| <= max B_ii <= 1 + K_ii, so its flag asks 1 + K_ii < 2^15 (fp16 overflows at 65504).
+// h3_now = any chain flagged (else the fp32-operand kernels launch), inv_any / inv_all likewise.
 void upload_h3(apm_ctx* c, int count) {
     int* h = pin_h3(c);
-    c->h3_now = false;
-    c->h3_all = count > 0;
+    int* v = pin_inv(c);
+    c->h3_now = c->inv_any = false;
+    c->h3_all = c->inv_all = count > 0;
     for (int b = 0; b < count; ++b) {
+        v[b] = v[b] && h[b];
         c->h3_now |= h[b] != 0;
         c->h3_all &= h[b] != 0;
+        c->inv_any |= v[b] != 0;
+        c->inv_all &= v[b] != 0;
     }
-    HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * count, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(c->h3post, pin_h3post(c), sizeof(int) * count, hipMemcpyHostToDevice,
+    const int B = c->max_batch;
+    HIPC(hipMemcpyAsync(c->h3ok, h, sizeof(int) * (2 * B + count), hipMemcpyHostToDevice,
                         c->stream));
     double* t = pin_icm(c);
-    for (int b = 0; b < count; ++b) t[b] = c->icm ? t[b] : -1.0;
+    for (int b = 0; b < count; ++b) t[b] = c->icm_q > 0.0 ? t[b] : -1.0;
     HIPC(hipMemcpyAsync(c->icm_thr, t, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
 }
 
@@ -900,9 +949,13 @@ void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true, bool 
     c->cholk_count = count;
     chol_k_panel(c, ex);
 }
+// edge cholk_rel[p] (main -> s2) carries no data: chol(K) works in BL, ldet + nb and the upper
+// half of Dinv, which nothing on the main stream touches while it runs (the fp64 Newton rerun,
+// which writes BL's first row block, drains it first); it only releases the panel behind the
+// main stream's TRSVs, whose single-workgroup-per-chain launches leave most CUs idle
 void feed_chol_k(apm_ctx* c) {
     if (c->cholk_next < 0 || c->cholk_next >= c->nb) return;
-    hipEvent_t e = c->ev_feed[c->feed_i++ & 3];
+    hipEvent_t e = c->ev.cholk_rel[c->cholk_next / c->outer];
     HIPC(hipEventRecord(e, c->stream));
     HIPC(hipStreamWaitEvent(c->stream2, e, 0));
     chol_k_panel(c, k_exec(c, c->stream2));
@@ -914,13 +967,14 @@ void chol_k_into_bl(apm_ctx* c, int count, const Exec& ex) {
     c->cholk_next = -1;
 }
 
-// enqueue what is left of the concurrent chol(K) and order the main stream behind it
+// enqueue what is left of the concurrent chol(K) and order the main stream behind it (edge
+// cholk_done, s2 -> main: L_K in BL, the log-dets in ldet + nb, status2)
 void drain_chol_k(apm_ctx* c) {
     if (c->cholk_next < 0) return;
     while (c->cholk_next < c->nb) chol_k_panel(c, k_exec(c, c->stream2));
     c->cholk_next = -1;
-    HIPC(hipEventRecord(c->ev_cholk, c->stream2));
-    HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
+    HIPC(hipEventRecord(c->ev.cholk_done, c->stream2));
+    HIPC(hipStreamWaitEvent(c->stream, c->ev.cholk_done, 0));
 }
 
 Exec k_exec(apm_ctx* c, hipStream_t s) {
@@ -968,35 +1022,37 @@ void post_bottom32_steps(apm_ctx* c, int count, int K, int Kend, hipStream_t s) 
     check_launch();
 }
 
-// APM_POST32=1: the whole bottom block after the fp64 factorisation of J M J, on the main stream
-void post_bottom32(apm_ctx* c, int count) {
-    const int nb = c->nb;
-    launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride, nb,
-                          c->outer, 0, nb, true, live_of(c), count, c->stream);
-    check_launch();
-    for (int K = 0; K < nb; K += c->outer)
-        post_bottom32_steps(c, count, K, std::min(K + c->outer, nb), c->stream);
-}
-
-// APM_POST32=2 (default): the bottom block's copy once L_K J is formed, then each outer panel of
-// the bottom on the low-priority stream2 as soon as the fp64 factorisation has finished that
-// panel of L' (post_bottom32_panel, chol_range's after_panel): the bottom's fp32 work fills the
-// CUs the fp64 in-panel steps leave idle instead of following the factorisation
+// The bottom block's copy once L_K J is formed, then each outer panel of the bottom on the
+// low-priority stream2 as soon as the fp64 factorisation has finished that panel of L'
+// (post_bottom32_panel, chol_range's after_panel): the bottom's fp32 work fills the CUs the fp64
+// in-panel steps leave idle instead of following the factorisation. Edge y2 (main -> s2): L_K J
+// in BL's fp64 rows, the chains' liveness (active reset by post_cov_lk).
 void post_bottom32_begin(apm_ctx* c, int count) {
-    HIPC(hipEventRecord(c->ev_gram, c->stream));
-    HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
+    HIPC(hipEventRecord(c->ev.y2, c->stream));
+    HIPC(hipStreamWaitEvent(c->stream2, c->ev.y2, 0));
     launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride,
                           c->nb, c->outer, 0, 0, true, live_of(c), count, c->stream2);
     check_launch();
 }
+// edge lp_panel[p] (main -> s2): the columns [K, Kend) of L' (rows K .. nb) and their diagonal
+// inverses (Dinv, first half) are final; the main stream's trailing update that follows writes
+// only columns >= Kend and Dinv[Kend]
 void post_bottom32_panel(apm_ctx* c, int count, int K, int Kend) {
-    hipEvent_t e = c->ev_feed[c->feed_i++ & 3];
+    hipEvent_t e = c->ev.lp_panel[K / c->outer];
     HIPC(hipEventRecord(e, c->stream));
     HIPC(hipStreamWaitEvent(c->stream2, e, 0));
     launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride,
                           c->nb, c->outer, K, Kend, false, live_of(c), count, c->stream2);
     check_launch();
     post_bottom32_steps(c, count, K, Kend, c->stream2);
+}
+
+// the guard (newton.hip k_guard_check) of the chains `lv` admits, after their slot write
+void guard_check(apm_ctx* c, Live lv, int count) {
+    launch_guard_check(c->ldet, c->lstride, c->nb, c->v.Kb, c->v.vstride, c->Sl, c->d_slots,
+                       c->guard, c->max_batch, GUARD_T1, GUARD_T2, GUARD_T3, GUARD_T4,
+                       c->guard_rows, c->v.f, APM_STATUS_GUARD, lv, count, c->stream);
+    check_launch();
 }
 
 // The fp64 bottom block for the chains flagged by the slot writer (bit 1 of Sl.chain_wide):
@@ -1014,8 +1070,9 @@ void bottom64_rerun(apm_ctx* c, int count, const std::vector<int>& redo) {
     chol_range(c, c->A, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, /*factor_diag=*/false,
                /*row_start=*/nb, y_gap, &ex);
     launch_slot_write(c->A, c->v, c->ldet, c->lstride, nb, c->Sl, c->d_slots, 2, c->n, c->np, lr,
-                      count, c->stream);
+                      count, c->stream, MatF{nullptr, 0, 0}, c->guard_rows);
     check_launch();
+    guard_check(c, lr, count);  // (the fp64 bottom's rows now: r3, r4 were skipped before)
     c->n_post64 += (int64_t)redo.size();
 }
 
@@ -1089,6 +1146,8 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
         chol_range(c, BL, 0, nb, nb + 1, nb, APM_STATUS_CHOL_K, count);       // L_K, h = L_K^-1 f
         launch_get_row(c->A, 2 * (int64_t)np, np, c->v.z, vs, lv, count, s);  // h -> z
         check_launch();
+        launch_guard_save(c->ldet, c->lstride, 0, nb, c->guard, c->max_batch, 1, lv, count, s);
+        check_launch();  // (1/2 log|K| before M's factorisation overwrites ldet[0, nb))
     }
     // J M J = I + Y2 Y2^T: on the 128x128 super-tile path one launch writes it without reading TL
     // (tile column j takes Y2's column blocks k <= j); otherwise TL starts as I and receives
@@ -1099,7 +1158,7 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
     // the bottom block's fp32 copy of L_K J (stream2, HBM-bound) beside the SYRK (MFMA-bound)
     // rather than beside the first panel's latency-bound in-panel steps (-1.4 ms per stationary
     // theta-call, profiles/r05_conv_early_ab.txt)
-    if (c->post32 == 2) post_bottom32_begin(c, count);
+    post_bottom32_begin(c, count);
     if (syrk1) {
         tracked_update(c, TL, nb, nb, 0, nb, 0, nb, Gap{0, 0}, 2, count);
     } else {
@@ -1110,23 +1169,17 @@ void post_cov_lk(apm_ctx* c, int count, bool have_lk = false) {
             tracked_update(c, TL, nb + K, Kend - K, K, nb, K, nb, Gap{0, 0}, 1, count);
         }
     }
-    if (!c->post32) {
-        chol_range(c, TL, 0, nb, 2 * nb, nb, APM_STATUS_CHOL_C, count, true, 0, y_gap);
-    } else if (c->post32 == 1) {  // J M J alone in fp64 (its log-determinant is log|B|)
-        chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count);
-    } else {  // ... with the fp32 bottom block following its panels on stream2
-        chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count, true, 0, no_gap, nullptr,
-                   nullptr, [c, count](int K, int Kend) { post_bottom32_panel(c, count, K, Kend); });
-    }
+    // J M J alone in fp64 (its log-determinant is log|B|), the fp32 bottom block following its
+    // panels on stream2
+    chol_range(c, TL, 0, nb, nb, nb, APM_STATUS_CHOL_C, count, true, 0, no_gap, nullptr, nullptr,
+               [c, count](int K, int Kend) { post_bottom32_panel(c, count, K, Kend); });
     launch_trmv_tiles(true, TL, c->v.z, c->v.Kb, vs, np, c->sympart, c->sstride, lv, count,
                       s);                                                     // g = J L'^T J h
     check_launch();
-    if (c->post32 == 1) {
-        post_bottom32(c, count);
-    } else if (c->post32 == 2) {  // the slot writer reads the bottom block: join stream2
-        HIPC(hipEventRecord(c->ev_cholk, c->stream2));
-        HIPC(hipStreamWaitEvent(c->stream, c->ev_cholk, 0));
-    }
+    // edge bottom_done (s2 -> main): the slot writer reads the bottom block (S32). APM_SKEW bit 2
+    // (tests only) drops this one wait, so that the skew test can show a missing edge being caught
+    HIPC(hipEventRecord(c->ev.bottom_done, c->stream2));
+    if (!(c->skew & 4)) HIPC(hipStreamWaitEvent(c->stream, c->ev.bottom_done, 0));
 }
 
 void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf, int* status,
@@ -1138,7 +1191,7 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
     HIPC(hipMemsetAsync(c->n_iter, 0, sizeof(int) * count, c->stream));
     reset_tickets(c);
     // IS: chol(K) runs on the second stream while the Newton iterations run on the main one
-    const bool ov = est == APM_EST_IS && c->mixed && c->overlap_k;
+    const bool ov = est == APM_EST_IS && c->mixed;
     // the matrix a factorisation of K starts from (chol(K)'s working copy BL, or PriorMC's A):
     // the Gram writes K's lower tiles there too instead of a later copy pass
     MatB k2{nullptr, 0, 0};
@@ -1177,23 +1230,40 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         u_eval_device(c, count, true);
     } else {
         if (ov) {
-            HIPC(hipEventRecord(c->ev_gram, c->stream));
-            HIPC(hipStreamWaitEvent(c->stream2, c->ev_gram, 0));
+            // edge gram_k (main -> s2): K and BL's first outer panel written by the Gram, the
+            // chains' theta (the statuses chol(K) keeps apart: status2 / active2)
+            HIPC(hipEventRecord(c->ev.gram_k, c->stream));
+            HIPC(hipStreamWaitEvent(c->stream2, c->ev.gram_k, 0));
             chol_k_begin(c, count, k_exec(c, c->stream2), /*copy=*/k2.base == nullptr,
                          /*partial=*/k2cols < c->nb);
         }
         const int64_t reruns = c->n_fp64_rerun;
-        if (est == APM_EST_LAPLACE)  // log|B| of the Newton factor itself: fp64 (lpa.py:116)
+        if (est == APM_EST_LAPLACE) {  // log|B| of the Newton factor itself: fp64 (lpa.py:116)
             newton(c, count, st_h, false, count);
-        else
+        } else {
             newton_is(c, count, st_h);
+            // the guard's 1/2 log|B| of the last Newton factor (k_guard_check)
+            launch_guard_save(c->ldet, c->lstride, 0, c->nb, c->guard, c->max_batch, 0, lv,
+                              count, c->stream);
+            check_launch();
+        }
         c->live_n = 0;
         for (int b = 0; b < count; ++b) c->live_n += st_h[b] == 0;
         if (ov) {
             drain_chol_k(c);  // what the TRSVs did not take (a no-op after an fp64 rerun)
             if (c->n_fp64_rerun != reruns)  // the fp64 Newton rerun used rows of BL: redo L_K
                 chol_k_into_bl(c, count, k_exec(c, c->stream));
+            // a chain whose blocked chol(K) failed is factored once more in LAPACK's dpotf2
+            // order (chol.hip k_chol_unblocked, n <= 512) before LinAlgError is raised: at the
+            // reference's InvalidCovarianceMatrixError thetas K's definiteness is decided by the
+            // rounding order
+            if (launch_chol_unblocked(c->K, bl_of(c), c->np, c->status2, APM_STATUS_CHOL_K,
+                                      c->ldet + c->nb, c->lstride, count, c->stream))
+                check_launch();
             launch_merge_status(c->status, c->status2, APM_STATUS_CHOL_K, count, c->stream);
+            check_launch();
+            launch_guard_save(c->ldet, c->lstride, c->nb, c->nb, c->guard, c->max_batch, 1, lv,
+                              count, c->stream);  // 1/2 log|K| (chol(K) on stream2: ldet + nb)
             check_launch();
         }
         if (est == APM_EST_LAPLACE) {
@@ -1203,8 +1273,9 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         } else {
             post_cov_lk(c, count, ov);
             launch_slot_write(c->A, c->v, c->ldet, c->lstride, c->nb, c->Sl, c->d_slots,
-                              c->post32 ? 3 : 2, c->n, c->np, lv, count, c->stream, s32_of(c));
+                              3, c->n, c->np, lv, count, c->stream, s32_of(c), c->guard_rows);
             check_launch();
+            guard_check(c, lv, count);
             u_eval_device(c, count, true);
         }
     }
@@ -1221,12 +1292,12 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
         const int64_t* hs = reinterpret_cast<const int64_t*>(c->hpin);  // the call's slots
         std::vector<int> chk;  // bit 3: the reference's route to chol(C) is checked (icm_check)
         for (int b = 0; b < count; ++b)
-            if (st_h[b] == 0 && (wide_h[b] & 8) && est == APM_EST_IS && c->icm) chk.push_back(b);
+            if (st_h[b] == 0 && (wide_h[b] & 8) && est == APM_EST_IS) chk.push_back(b);
         std::vector<int> redo, rewrite;  // fp32 bottom blocks above the trace bound (bit 1);
         bool attached = false;           // wide slots whose fp64 factor was not written (bit 2)
-        for (int b = 0; b < count; ++b) {
-            if (st_h[b] != 0) continue;
-            const bool rd = (wide_h[b] & 2) && est == APM_EST_IS;
+        for (int b = 0; b < count; ++b) {  // (a guard-failed chain's slot was written too)
+            if (st_h[b] != 0 && st_h[b] != APM_STATUS_GUARD) continue;
+            const bool rd = (wide_h[b] & 2) && est == APM_EST_IS && st_h[b] == 0;
             if (rd) redo.push_back(b);
             if ((wide_h[b] & 4) && !c->l64_h[hs[b]]) {
                 attach_l64(c, hs[b]);
@@ -1252,13 +1323,18 @@ void theta_eval_impl(apm_ctx* c, int est, int count, bool gram, double* out_logf
                           RB{c->status, (int)sizeof(int) * count, st_h.data()},
                           RB{c->Sl.chain_wide, (int)sizeof(int) * count, wide_h.data()}});
         }
+        // the slots as the slot writer left them: the host mirror (slot_wide, the fp64 factor
+        // attachments) follows every slot written this call, also of a chain the reference-route
+        // check fails below (its slot holds a complete state that no caller reads)
+        const std::vector<int> st_slot = st_h;
         if (!chk.empty()) {  // (after everything that reads A)
             icm_check(c, count, chk);
             read_back(c, {RB{c->status, (int)sizeof(int) * count, st_h.data()}});
         }
+        for (int b = 0; b < count; ++b) c->n_guard += st_h[b] == APM_STATUS_GUARD;
         bool detached = false;
         for (int b = 0; b < count; ++b) {
-            if (st_h[b] != 0) continue;
+            if (st_slot[b] != 0 && st_slot[b] != APM_STATUS_GUARD) continue;
             c->slot_wide[hs[b]] = wide_h[b] & 1;
             if (!(wide_h[b] & 1) && c->l64_h[hs[b]]) {
                 detach_l64(c, hs[b]);
@@ -1290,42 +1366,47 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
               int64_t ldx, const double* y, double eps, int64_t S, int64_t max_batch,
               int64_t n_slots, int64_t n_ubufs) {
     c->device = device;
-    // development knobs, read here once per context; defaults are the measured best
-    if (const char* e = getenv("APM_OUTER")) c->outer = std::max(1, atoi(e));
+    // the library's environment knobs, read here once per context: two
+    // correctness fallbacks (APM_MIXED=0: fp64 Newton factorisation; APM_H3=0: fp32 operands in
+    // the fp32 factorisations' outer updates) and test thresholds / test modes that the GPU
+    // tests use to reach rare paths. The defaults are the product.
     HIPC(hipSetDevice(device));
     trsv32_mw_init();
     if (const char* e = getenv("APM_MIXED")) c->mixed = atoi(e) != 0;
-    if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
-    if (const char* e = getenv("APM_OVERLAP_K")) c->overlap_k = atoi(e) != 0;
     if (const char* e = getenv("APM_H3")) c->h3 = atoi(e) != 0;
-    if (const char* e = getenv("APM_DF32")) c->df32 = atoi(e) != 0;
-    if (const char* e = getenv("APM_POST32")) c->post32 = std::max(0, std::min(2, atoi(e)));
-    if (const char* e = getenv("APM_LOOKAHEAD")) c->lookahead = atoi(e) != 0;
-    if (const char* e = getenv("APM_PLANES")) c->planes_on = atoi(e) != 0;
-    if (const char* e = getenv("APM_Q256")) c->q256 = atoi(e) != 0;
-    if (const char* e = getenv("APM_DFINV")) c->dfinv = atoi(e) != 0;
-    if (const char* e = getenv("APM_SYMV_TPW")) c->symv_tpw = atoi(e);
-    if (const char* e = getenv("APM_ICM")) c->icm = atoi(e) != 0;
-    if (const char* e = getenv("APM_ICM_Q")) c->icm_q = std::max(1.0, atof(e));
-    // test knob: poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces
-    // the bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
+    // acceptance of a refinement step (test threshold: 0 sends every chain to the fp64 rerun)
+    if (const char* e = getenv("APM_REFINE_TOL")) c->refine_tol = atof(e);
+    // the reference-route check of chol(C) (icm_check): trace(C) below n K_ii / APM_ICM_Q
+    // (test threshold: 1 checks every chain, 0 none)
+    if (const char* e = getenv("APM_ICM_Q")) c->icm_q = std::max(0.0, atof(e));
+    // poll bound of every in-launch hand-over wait (tests/test_gpu_errors.py forces the
+    // bounded-spin exits with 1 and checks that no chain returns a wrong value with status 0)
     if (const char* e = getenv("APM_SPIN_LIMIT")) c->spin_df = c->spin_trsv = std::max(1, atoi(e));
+    // delay kernels in front of every launch on the secondary streams (bit 0) and/or on the main
+    // stream (bit 1): a cross-stream edge without its wait then gives a wrong result
+    // deterministically (tests/test_gpu_errors.py::test_stream_skew_is_bitwise_neutral); bit 2
+    // removes one edge's wait (bottom_done) to show that such a result is caught
+    if (const char* e = getenv("APM_SKEW")) c->skew = std::max(0, std::min(7, atoi(e)));
     {  // main stream at the highest priority: the concurrent chol(K) only fills idle CUs
         int least = 0, greatest = 0;
         HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPC(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
         HIPC(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, least));
         HIPC(hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, least));
-        for (hipEvent_t& e : c->ev_la) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIPC(hipEventCreateWithFlags(&c->ev_gram, hipEventDisableTiming));
-        HIPC(hipEventCreateWithFlags(&c->ev_cholk, hipEventDisableTiming));
-        for (hipEvent_t& e : c->ev_feed) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     c->kind = kind;
     c->n = (int)n;
     c->d = (int)d;
     c->np = (int)((n + 63) / 64 * 64);
     c->nb = c->np / 64;
+    {  // one event per cross-stream edge (Edges): the per-panel ones indexed by panel
+        const int np64 = (c->nb + c->outer - 1) / c->outer, np32 = (c->nb + c->outer32 - 1) / c->outer32;
+        c->ev.cholk_rel.assign(np64, nullptr);
+        c->ev.lp_panel.assign(np64, nullptr);
+        c->ev.df.assign(np32, nullptr);
+        c->ev.far.assign(np32, nullptr);
+        for (hipEvent_t* e : c->ev.all()) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
     c->P = kind == APM_KERNEL_ISO ? 2 : (kind == APM_KERNEL_ARD ? (int)d + 1 : 0);
     c->S = (int)S;
     c->sp = (int)((S + 63) / 64 * 64);
@@ -1376,21 +1457,25 @@ void init_ctx(apm_ctx* c, int device, int kind, const double* X, int64_t n, int6
     c->refine_prev = dalloc<double>(c, B);
     c->d_slots = dalloc<int64_t>(c, 2 * B);
     c->d_ubufs = c->d_slots + B;
-    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 32, hipHostMallocDefault));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)B * 40, hipHostMallocDefault));
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hmask), sizeof(int) * (size_t)B,
                        hipHostMallocDefault));
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->hx), (size_t)B * 20,
                        hipHostMallocMapped | hipHostMallocCoherent));
     HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->dx), c->hx, 0));
-    c->h3ok = dalloc<int>(c, 2 * B);
+    c->h3ok = dalloc<int>(c, 3 * B);
     c->h3post = c->h3ok + B;
+    c->invok = c->h3ok + 2 * B;
+    c->guard = dalloc<double>(c, 6 * B);
+    HIPC(hipMemset(c->guard, 0, sizeof(double) * 6 * B));
+    c->guard_rows = dalloc<double>(c, B * np);
     c->icm_thr = dalloc<double>(c, B);
     // + 3: the bounded-spin timeouts of the dataflow panel (APM_PROF_DF_TIMEOUTS) and of the
     // TRSV (APM_PROF_TRSV_TIMEOUTS), the arrival-ticket counter (spin_words)
-    if (c->mixed && c->df32 && c->h3 && c->planes_on) {
+    if (c->mixed && c->h3) {
         c->plane_cs = 2 * np * 32 * 2 * c->outer32;  // 2 planes x rows x 2 outer32 slices x 32
         c->planes = dalloc<unsigned short>(c, 2 * B * c->plane_cs);
-        if (c->dfinv && c->outer32 == 8) {
+        {
             c->zt = dalloc<float>(c, B * 3 * 512 * 512);
             c->zplanes = dalloc<unsigned short>(c, B * 2 * 16 * 512 * 32);
         }
@@ -1447,14 +1532,10 @@ void free_ctx(apm_ctx* c) {
     if (c->hmask) (void)hipHostFree(c->hmask);
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
-    for (hipEvent_t e : c->ev_la)
-        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t* e : c->ev.all())
+        if (*e) (void)hipEventDestroy(*e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    if (c->ev_gram) (void)hipEventDestroy(c->ev_gram);
-    if (c->ev_cholk) (void)hipEventDestroy(c->ev_cholk);
-    for (hipEvent_t e : c->ev_feed)
-        if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -1518,6 +1599,7 @@ void* apm_stream(apm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 int apm_u_upload(apm_ctx* c, int64_t ubuf, const double* U, int64_t ldu) {
     if (!c || !U || ubuf < 0 || ubuf >= c->n_ubufs || ldu < c->S)
         return fail(c, APM_E_INVALID, "apm_u_upload: bad arguments");
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         HIPC(hipMemcpy2DAsync(c->U64, sizeof(double) * c->S, U, sizeof(double) * ldu,
@@ -1553,6 +1635,7 @@ int apm_u_normal(apm_ctx* c, int64_t count, const int64_t* ubufs, const uint64_t
     if (!c || count <= 0 || count > c->max_batch || !ubufs || !seeds || !counters)
         return fail(c, APM_E_INVALID, "apm_u_normal: bad arguments");
     if (!check_idx(c, count, ubufs, c->n_ubufs, "ubuf")) return APM_E_INVALID;
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         const int64_t B = c->max_batch;
@@ -1578,6 +1661,7 @@ int apm_u_combine(apm_ctx* c, int64_t count, const int64_t* dst, const int64_t* 
     if (!check_idx(c, count, dst, c->n_ubufs, "dst") || !check_idx(c, count, a, c->n_ubufs, "a") ||
         !check_idx(c, count, b, c->n_ubufs, "b"))
         return APM_E_INVALID;
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         const int64_t B = c->max_batch;
@@ -1610,6 +1694,7 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
             !check_idx(c, count, ubufs, c->n_ubufs, "ubuf"))
             return APM_E_INVALID;
     }
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         double* th = c->hth;  // pinned: the upload is asynchronous
@@ -1621,8 +1706,9 @@ int apm_theta_eval(apm_ctx* c, int est, int64_t count, const double* thetas, int
         // the posterior bottom block's operands |L'_ij| <= sqrt(1 + n K_ii) (postcov.hip)
         for (int64_t b = 0; b < count; ++b) {
             pin_h3(c)[b] = c->h3 && th[b * c->P] < 19.0;
+            pin_inv(c)[b] = 1.0 + std::exp(th[b * c->P]) + c->eps < 32768.0;
             pin_h3post(c)[b] = c->h3 && 1.0 + c->n * (std::exp(th[b * c->P]) + c->eps) < 4e8;
-            pin_icm(c)[b] = c->n * (std::exp(th[b * c->P]) + c->eps) / c->icm_q;  // K_ii
+            pin_icm(c)[b] = c->n * (std::exp(th[b * c->P]) + c->eps) / std::max(c->icm_q, 1.0);
         }
         upload_h3(c, (int)count);
         if (est != APM_EST_LAPLACE) upload_idx(c, (int)count, slots, ubufs);
@@ -1640,6 +1726,7 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
     if (est != APM_EST_LAPLACE &&
         (slot < 0 || slot >= c->n_slots || ubuf < 0 || ubuf >= c->n_ubufs))
         return fail(c, APM_E_INVALID, "apm_theta_eval_K: slot/ubuf out of range");
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         // identity-padded copy of K into chain 0's K
@@ -1654,8 +1741,9 @@ int apm_theta_eval_K(apm_ctx* c, int est, const double* K, int64_t ldk, int64_t 
         double kmax = 0.0;
         for (int i = 0; i < c->n; ++i) kmax = std::max(kmax, std::fabs(Kp[(size_t)i * c->np + i]));
         pin_h3(c)[0] = c->h3 && kmax < 1.8e8;  // sqrt(1 + K_ii) < 1.4e4 (chol32.hip)
+        pin_inv(c)[0] = 1.0 + kmax < 32768.0;
         pin_h3post(c)[0] = c->h3 && 1.0 + c->n * kmax < 4e8;
-        pin_icm(c)[0] = c->n * kmax / c->icm_q;
+        pin_icm(c)[0] = c->n * kmax / std::max(c->icm_q, 1.0);
         upload_h3(c, 1);
         upload_idx(c, 1, &slot, &ubuf);  // (the pinned copy is the slot the read-back marks)
         theta_eval_impl(c, est, 1, false, out_logf, status, nops);
@@ -1672,6 +1760,7 @@ int apm_u_eval(apm_ctx* c, int64_t count, const int64_t* slots, const int64_t* u
     if (!check_idx(c, count, slots, c->n_slots, "slot") ||
         !check_idx(c, count, ubufs, c->n_ubufs, "ubuf"))
         return APM_E_INVALID;
+    const SkewScope skew(c);
     try {
         HIPC(hipSetDevice(c->device));
         upload_idx(c, (int)count, slots, ubufs);
@@ -1908,6 +1997,23 @@ int apm_selftest_philox(int device, int64_t n, const uint32_t* in, uint32_t* out
     return APM_SUCCESS;
 }
 
+int apm_guard_read(apm_ctx* c, int64_t count, double* r) {
+    if (!c || !r || count <= 0 || count > c->max_batch)
+        return fail(c, APM_E_INVALID, "apm_guard_read: bad arguments");
+    try {
+        HIPC(hipSetDevice(c->device));
+        std::vector<double> h((size_t)4 * c->max_batch);
+        HIPC(hipMemcpyAsync(h.data(), c->guard + 2 * c->max_batch, sizeof(double) * h.size(),
+                            hipMemcpyDeviceToHost, c->stream));
+        sync(c);
+        for (int64_t b = 0; b < count; ++b)
+            for (int k = 0; k < 4; ++k) r[4 * b + k] = h[(size_t)k * c->max_batch + b];
+    } catch (const HipError& e) {
+        return fail(c, APM_E_HIP, e.msg);
+    }
+    return APM_SUCCESS;
+}
+
 int apm_prof_enable(apm_ctx* c, int on) {
     if (!c) return fail(c, APM_E_INVALID, "apm_prof_enable: null ctx");
     c->prof = on < 0 ? 0 : (on > 2 ? 2 : on);
@@ -1948,6 +2054,14 @@ int apm_prof_read(apm_ctx* c, int kind, double* total_ms, int64_t* launches, dou
             if (launches) *launches = c->n_post64;
             if (work) *work = 0.0;
             if (reset) c->n_post64 = 0;
+            return APM_SUCCESS;
+        }
+        if (kind == APM_PROF_ICM_CHECKS || kind == APM_PROF_GUARD) {
+            int64_t& n = kind == APM_PROF_GUARD ? c->n_guard : c->n_icm_check;
+            if (total_ms) *total_ms = 0.0;
+            if (launches) *launches = n;
+            if (work) *work = 0.0;
+            if (reset) n = 0;
             return APM_SUCCESS;
         }
         if (kind == APM_PROF_STATS) {

@@ -224,7 +224,7 @@ void launch_chol_panel32(MatF A, int k, int i0, int R, int glo, int ghi, const f
     if (ghi <= glo) glo = ghi = R;
     const int rows = (R - i0) - (ghi - glo);
     if (rows <= 0) return;
-    hipLaunchKernelGGL(k_chol_panel32, dim3(rows, nchains), dim3(256), 0, s, A, k, i0, glo, ghi,
+    APM_LAUNCH(k_chol_panel32, dim3(rows, nchains), dim3(256), 0, s, A, k, i0, glo, ghi,
                        Dinv, dstride, live);
 }
 
@@ -309,7 +309,7 @@ void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int nti
                           const int* h3ok) {
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
-    hipLaunchKernelGGL(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
+    APM_LAUNCH(k_chol_update32, dim3((unsigned)total), dim3(256), 0, s, A, k0, kc, tiles,
                        ntiles, nchains, live, fd, hlim, h3ok);
 }
 
@@ -389,7 +389,8 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
                                                          int64_t pstride,
                                                          unsigned long long base, SpinCtl sc,
                                                          Planes16 pl, int rhs_as = -1,
-                                                         bool inv_skip = false, int row0 = 0,
+                                                         const int* __restrict__ inv_skip = nullptr,
+                                                         int row0 = 0,
                                                          int zrow = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
     __shared__ union {
@@ -433,9 +434,10 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
         // explicit-inverse panels (k_panel_inv_gemm32): this launch walks the diagonal block and
         // the right-hand-side row only, the last logical row being that row
         if (rhs_as >= 0 && i == Kend) i = rhs_as;
-        // ... or the whole panel, the rows below the diagonal block of the fp16x3 chains excepted
-        // (a batch with a chain outside fp16's range: those chains walk, the others do not)
-        if (inv_skip && i >= Kend && i < hlim && (!h3ok || h3ok[b])) return;
+        // ... or the whole panel, the rows below the diagonal block of the chains that take the
+        // explicit-inverse panel excepted (inv_skip: the host's invok flags; a batch with a chain
+        // outside their range: that chain walks, the others do not)
+        if (inv_skip && i >= Kend && i < hlim && inv_skip[b]) return;
     }
     const bool pub = !BULK && i < Kend;  // rows of the diagonal block: later rows wait on them
     unsigned long long* pr = prog + b * pstride;
@@ -657,13 +659,13 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
 long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd, Live live,
                             int nchains, int hlim, const int* h3ok, unsigned long long* prog,
                             int64_t pstride, unsigned long long base, SpinCtl sc, hipStream_t s,
-                            Planes16 pl, int rhs_as, bool inv_skip) {
+                            Planes16 pl, int rhs_as, const int* inv_skip) {
     // the progress word holds the step in 4 bits, 15 = failed: a wider panel is refused (the
     // caller raises) instead of being left unfactored
     if (ncols > 14) return -1;
     if (ncols < 1 || R - K <= 1) return 0;  // (one column: its panel TRSM)
     const long grid = (long)(R - K) * nchains;
-    hipLaunchKernelGGL(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
+    APM_LAUNCH(k_chol_panel_df32<false>, dim3((unsigned)grid), dim3(256), 0, s, A, K,
                        ncols, R, nchains, fd, live, hlim, h3ok, prog, pstride, base, sc, pl,
                        rhs_as, inv_skip);
     return grid;
@@ -673,10 +675,10 @@ void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zro
                               FusedDiag<float> fd, Live live, int nchains, int hlim,
                               const int* h3ok, hipStream_t s) {
     if (ncols < 1 || R <= row0) return;
-    hipLaunchKernelGGL(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
+    APM_LAUNCH(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
                        (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0},
-                       Planes16{nullptr, 0, 0, 0}, -1, false, row0, zrow);
+                       Planes16{nullptr, 0, 0, 0}, -1, (const int*)nullptr, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -1083,7 +1085,7 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
     if (ntiles <= 0) return;
     const long total = (long)ntiles * nchains;
 #define UPD32_LAUNCH(H, R)                                                                     \
-    hipLaunchKernelGGL((k_chol_update32_t128<H, R>), dim3((unsigned)total), dim3(256), 0, s, A, \
+    APM_LAUNCH((k_chol_update32_t128<H, R>), dim3((unsigned)total), dim3(256), 0, s, A, \
                        k0, kc, tiles, ntiles, nchains, live, fd, H ? hlim : 0,               \
                        H ? h3ok : nullptr, rhs, pl)
     if (hlim > 0) {
@@ -1224,7 +1226,7 @@ __global__ __launch_bounds__(512, 1) void k_chol_update32_q256(MatF A, int k0, i
 void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, int nq, Live live,
                                int nchains, hipStream_t s, const int* h3ok, Planes16 pl) {
     if (nq <= 0 || !pl.base) return;
-    hipLaunchKernelGGL(k_chol_update32_q256, dim3((unsigned)((long)nq * nchains)), dim3(512), 0, s,
+    APM_LAUNCH(k_chol_update32_q256, dim3((unsigned)((long)nq * nchains)), dim3(512), 0, s,
                        A, k0, kc, quads, nq, nchains, live, h3ok, pl);
 }
 
@@ -1480,11 +1482,11 @@ void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstrid
                         int64_t zstride, Planes16 zpl, Planes16 pl, Live live, int nchains,
                         const int* h3ok, hipStream_t s) {
     for (int m = 1; m <= 4; m *= 2)
-        hipLaunchKernelGGL(k_zinv_level32, dim3((unsigned)(4 * nchains)), dim3(256), 0, s, A, K,
+        APM_LAUNCH(k_zinv_level32, dim3((unsigned)(4 * nchains)), dim3(256), 0, s, A, K,
                            m, Dinv, dstride, zt, zstride, zpl, live, h3ok);
     const int Kend = K + 8;
     if (nb > Kend)
-        hipLaunchKernelGGL(k_panel_inv_gemm32,
+        APM_LAUNCH(k_panel_inv_gemm32,
                            dim3((unsigned)((long)((nb - Kend + 1) / 2) * nchains)), dim3(512), 0,
                            s, A, K, Kend, nb, zpl, pl, live, nchains, h3ok);
 }
@@ -1563,7 +1565,7 @@ __global__ __launch_bounds__(256) void k_row32(MatF Bf, int64_t row, int np, dou
 
 void launch_row32(MatF Bf, int64_t row, int np, double* out, int64_t ostride, Live live,
                   int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_row32, dim3((np + 255) / 256, nchains), dim3(256), 0, s, Bf, row, np,
+    APM_LAUNCH(k_row32, dim3((np + 255) / 256, nchains), dim3(256), 0, s, Bf, row, np,
                        out, ostride, live);
 }
 
@@ -1719,15 +1721,15 @@ void launch_symv(MatB K, const double* x, int64_t xstride, double* y, int64_t ys
                  int64_t wstride, Live live, int nchains, hipStream_t s, int symv_tpw) {
     const int nb = np / 64, nt = nb * (nb + 1) / 2;
     if (symv_tpw >= 4)
-        hipLaunchKernelGGL(k_symv_part<4>, dim3((nt + 3) / 4, nchains), dim3(256), 0, s, K, x,
+        APM_LAUNCH(k_symv_part<4>, dim3((nt + 3) / 4, nchains), dim3(256), 0, s, K, x,
                            xstride, part, pstride, nb, Bf, Ws, wstride, live);
     else if (symv_tpw == 2)
-        hipLaunchKernelGGL(k_symv_part<2>, dim3((nt + 1) / 2, nchains), dim3(256), 0, s, K, x,
+        APM_LAUNCH(k_symv_part<2>, dim3((nt + 1) / 2, nchains), dim3(256), 0, s, K, x,
                            xstride, part, pstride, nb, Bf, Ws, wstride, live);
     else
-        hipLaunchKernelGGL(k_symv_part<1>, dim3(nt, nchains), dim3(256), 0, s, K, x, xstride,
+        APM_LAUNCH(k_symv_part<1>, dim3(nt, nchains), dim3(256), 0, s, K, x, xstride,
                            part, pstride, nb, Bf, Ws, wstride, live);
-    hipLaunchKernelGGL(k_symv_reduce, dim3((np + 255) / 256, nchains), dim3(256), 0, s, part,
+    APM_LAUNCH(k_symv_reduce, dim3((np + 255) / 256, nchains), dim3(256), 0, s, part,
                        pstride, nb, y, ystride, Bf, Ws, wstride, live);
 }
 
@@ -2026,26 +2028,26 @@ long launch_trsv32_mw(bool fwd, MatF A, int nb, const float* Dinv, int64_t dstri
     const size_t lds = sizeof(double) * (nb * 64 + 4 * 64 + 64);
     const int np = nb * 64;
     const int G = TRM_G;
-    hipLaunchKernelGGL(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,
+    APM_LAUNCH(k_nan_fill, dim3((np + 255) / 256, nchains), dim3(256), 0, s, out, vstride,
                        np, live);
     if (fwd)
-        hipLaunchKernelGGL(k_trsv32_mw<true>, dim3(nchains * G), dim3(256), lds, s, A, nb,
+        APM_LAUNCH(k_trsv32_mw<true>, dim3(nchains * G), dim3(256), lds, s, A, nb,
                            Dinv, dstride, r, out, vstride, live, fail_code, G, nchains, sc);
     else
-        hipLaunchKernelGGL(k_trsv32_mw<false>, dim3(nchains * G), dim3(256), lds, s, A, nb,
+        APM_LAUNCH(k_trsv32_mw<false>, dim3(nchains * G), dim3(256), lds, s, A, nb,
                            Dinv, dstride, r, out, vstride, live, fail_code, G, nchains, sc);
     return (long)nchains * G;
 }
 
 void launch_trsv_fwd32(MatF A, int J, int nb, const float* Dinv, int64_t dstride, double* r,
                        double* y, int64_t vstride, Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_trsv_fwd32, dim3(nb - J, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
+    APM_LAUNCH(k_trsv_fwd32, dim3(nb - J, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
                        r, y, vstride, live);
 }
 
 void launch_trsv_bwd32(MatF A, int J, const float* Dinv, int64_t dstride, double* r, double* z,
                        int64_t vstride, Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_trsv_bwd32, dim3(J + 1, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
+    APM_LAUNCH(k_trsv_bwd32, dim3(J + 1, nchains), dim3(256), 0, s, A, J, Dinv, dstride,
                        r, z, vstride, live);
 }
 
@@ -2118,7 +2120,7 @@ __global__ __launch_bounds__(256) void k_refine_check(const double* __restrict__
 void launch_refine_check(const double* x, const double* d, int64_t vstride, int np, double tol,
                          int fail_code, int step, bool last, double* prev, int* refining,
                          const int* status, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_refine_check, dim3(nchains), dim3(256), 0, s, x, d, vstride, np, tol,
+    APM_LAUNCH(k_refine_check, dim3(nchains), dim3(256), 0, s, x, d, vstride, np, tol,
                        fail_code, step, (int)last, prev, refining,
                        Live{refining, const_cast<int*>(status)});
 }
@@ -2129,12 +2131,12 @@ __global__ void k_refine_mask(Live live, int* refining, int nchains) {
 }
 
 void launch_refine_mask(Live live, int* refining, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_refine_mask, dim3((nchains + 255) / 256), dim3(256), 0, s, live,
+    APM_LAUNCH(k_refine_mask, dim3((nchains + 255) / 256), dim3(256), 0, s, live,
                        refining, nchains);
 }
 
 void launch_refine(int mode, const double* Ws, const double* Kb, double* x, const double* Kt,
                    double* out, int64_t vstride, int np, Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_refine, dim3((np + 255) / 256, nchains), dim3(256), 0, s, mode, Ws, Kb,
+    APM_LAUNCH(k_refine, dim3((np + 255) / 256, nchains), dim3(256), 0, s, mode, Ws, Kb,
                        x, Kt, out, vstride, np, live);
 }

@@ -143,6 +143,6 @@ void launch_gram(MatB K, const double* X, int64_t ldx, int n, int d, const doubl
                  int64_t tstride, int kind, double eps, int np, Live live, int nchains,
                  hipStream_t s, bool both, MatB K2, int k2cols) {
     const int nb = np / 64, ns = (nb + 1) / 2;
-    hipLaunchKernelGGL(k_gram, dim3(ns * (ns + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx, n, d,
+    APM_LAUNCH(k_gram, dim3(ns * (ns + 1) / 2, nchains), dim3(256), 0, s, K, X, ldx, n, d,
                        theta, tstride, kind, eps, live, (int)both, K2, k2cols, nb);
 }

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void k_newton_prep(NewtonVecs v, const double*
 
 void launch_newton_prep(NewtonVecs v, const double* y, int n, int np, Live live, int nchains,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_newton_prep, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, y, n,
+    APM_LAUNCH(k_newton_prep, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, y, n,
                        np, live);
 }
 
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_gemv(MatB M, const double* __restrict__
 
 void launch_gemv(MatB M, const double* x, int64_t xstride, double* out, int64_t ostride, int np,
                  Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_gemv, dim3(np / 16, nchains), dim3(256), 0, s, M, x, xstride, out,
+    APM_LAUNCH(k_gemv, dim3(np / 16, nchains), dim3(256), 0, s, M, x, xstride, out,
                        ostride, np, live);
 }
 
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void k_form_B(MatB K, MatB A, NewtonVecs v, in
 
 void launch_form_B(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains, hipStream_t s) {
     const int nb = np / 64;
-    hipLaunchKernelGGL(k_form_B, dim3(nb * (nb + 1) / 2 + nb, nchains), dim3(256), 0, s, K, A, v,
+    APM_LAUNCH(k_form_B, dim3(nb * (nb + 1) / 2 + nb, nchains), dim3(256), 0, s, K, A, v,
                        nb, live);
 }
 
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_newton_update(NewtonVecs v, int np, Liv
 }
 
 void launch_newton_update(NewtonVecs v, int np, Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_newton_update, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, np,
+    APM_LAUNCH(k_newton_update, dim3((np + 255) / 256, nchains), dim3(256), 0, s, v, np,
                        live);
 }
 
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_newton_check(NewtonVecs v, int n, int n
 
 void launch_newton_check(NewtonVecs v, int n, int np, double tol, int* active, const int* status,
                          int* n_iter, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_newton_check, dim3(nchains), dim3(256), 0, s, v, n, np, tol, active,
+    APM_LAUNCH(k_newton_check, dim3(nchains), dim3(256), 0, s, v, n, np, tol, active,
                        status, n_iter);
 }
 
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_copy_lower(MatB src, MatB dst, Live liv
 
 void launch_copy_lower(MatB src, MatB dst, int np, Live live, int nchains, hipStream_t s) {
     const int nb = np / 64;
-    hipLaunchKernelGGL(k_copy_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, src, dst,
+    APM_LAUNCH(k_copy_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, src, dst,
                        live);
 }
 
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void k_form_aug(MatB K, MatB A, NewtonVecs v, 
 void launch_form_aug(MatB K, MatB A, NewtonVecs v, int np, Live live, int nchains,
                      hipStream_t s, bool lower_only) {
     const int nb = np / 64;
-    hipLaunchKernelGGL(k_form_aug, dim3(nb * nb + nb * (nb + 1) / 2 + 2 * nb, nchains), dim3(256),
+    APM_LAUNCH(k_form_aug, dim3(nb * nb + nb * (nb + 1) / 2 + 2 * nb, nchains), dim3(256),
                        0, s, K, A, v, nb, live, (int)lower_only);
 }
 
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_laplace_lml(NewtonVecs v, const double*
 void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet,
                         int64_t lstride, int nb, double* out, Live live, int nchains,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_laplace_lml, dim3(nchains), dim3(256), 0, s, v, y, n, ldet, lstride, nb,
+    APM_LAUNCH(k_laplace_lml, dim3(nchains), dim3(256), 0, s, v, y, n, ldet, lstride, nb,
                        out, live);
 }
 
@@ -270,10 +270,16 @@ void launch_laplace_lml(NewtonVecs v, const double* y, int n, const double* ldet
 // mode 2 (IS, chol(K)):   L = (block at rows np.., cols 0..) J, row np = g^T (vector v.Kb)
 // Rows are written whole (upper part zero) because the u-path GEMM streams full row segments.
 // mode 3 (IS, fp32 bottom): L = (rows np.. of S32) J, row np = g^T
+// mode 2 / 3 also write the guard's row residuals e_r = (C_chol g)_r - f_post_r (fp32 factor
+// row, fp64 g = C_chol^-1 f_post from the fp64 posterior factors and f_post from the Newton
+// vectors; k_guard_check): every row of the factor is checked against two fp64 quantities it
+// was not computed from, so a tile of C_chol that was read before it was final shows
 __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
                                                       const int64_t* __restrict__ slots, int mode,
                                                       int np, const double* __restrict__ gvec,
-                                                      int64_t gstride, Live live, MatF S32) {
+                                                      int64_t gstride, Live live, MatF S32,
+                                                      const double* __restrict__ fvec,
+                                                      double* rowe) {
     const int b = blockIdx.y;
     if (live.status[b] != 0 || live.active[b] == 0) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -281,15 +287,18 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     const double* Ab = A.base + b * A.cstride;
     float* L = S.L + slots[b] * S.lstride + (int64_t)r * np;
     double q = 0.0;  // squared norm of factor row r (the wide-slot test, k_slot_write_vec)
+    double pg = 0.0;  // (C_chol g)_r of the fp32 row (the guard)
     // rows stop at the end of their diagonal tile: k_ugemm reads row r up to column
     // 64 (r / 64 + 1) only (apm_slot_read zeroes the rest on the host)
     const int cend = (r / 64 + 1) * 64;
+    const double* g = gvec + b * gstride;
     if (r < np && mode == 3) {  // as mode 2, from the fp32 bottom block
         const float* src = S32.base + b * S32.cstride + ((int64_t)np + r) * S32.ld;
         for (int c = lane; c < cend; c += 64) {
             const float x = (c <= r) ? src[np - 1 - c] : 0.0f;
             L[c] = x;
             q += (double)x * (double)x;
+            pg += (double)x * g[c];
         }
     } else if (r < np && mode == 2) {  // chol(C) = (chol(C) J) J: row r of the block at (np, 0), reversed
         const double* src = Ab + ((int64_t)np + r) * A.ld;
@@ -297,6 +306,7 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
             const double x = (c <= r) ? src[np - 1 - c] : 0.0;
             L[c] = (float)x;
             q += x * x;
+            pg += (double)(float)x * g[c];
         }
     } else if (r < np) {
         const double* src = Ab + (int64_t)r * A.ld;
@@ -314,6 +324,10 @@ __global__ __launch_bounds__(256) void k_slot_write_L(MatB A, SlotSet S,
     if (r < np) {
         q = wave_sum_d(q);
         if (lane == 0) S.rowq[slots[b] * S.vstride + r] = q;
+        if (mode >= 2 && rowe) {
+            pg = wave_sum_d(pg);
+            if (lane == 0) rowe[b * (int64_t)np + r] = pg - fvec[b * gstride + r];
+        }
     }
 }
 
@@ -389,17 +403,17 @@ __global__ __launch_bounds__(256) void k_slot_write_vec(MatB A, NewtonVecs v, co
 
 void launch_slot_write(MatB A, NewtonVecs v, const double* ldet, int64_t lstride, int nb,
                        SlotSet S, const int64_t* slots, int mode, int n, int np, Live live,
-                       int nchains, hipStream_t s, MatF S32) {
-    hipLaunchKernelGGL(k_slot_write_L, dim3((np + 64) / 4, nchains), dim3(256), 0, s, A, S, slots,
-                       mode, np, v.Kb, v.vstride, live, S32);
-    hipLaunchKernelGGL(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
+                       int nchains, hipStream_t s, MatF S32, double* rowe) {
+    APM_LAUNCH(k_slot_write_L, dim3((np + 64) / 4, nchains), dim3(256), 0, s, A, S, slots,
+                       mode, np, v.Kb, v.vstride, live, S32, (const double*)v.f, rowe);
+    APM_LAUNCH(k_slot_write_vec, dim3(nchains), dim3(256), 0, s, A, v, ldet, lstride, nb,
                        S, slots, mode, n, live);
     launch_slot_write_L64(A, S, slots, mode, np, live, nchains, s);
 }
 
 void launch_slot_write_L64(MatB A, SlotSet S, const int64_t* slots, int mode, int np, Live live,
                            int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_slot_write_L64, dim3(np / 4, nchains), dim3(256), 0, s, A, S, slots, mode,
+    APM_LAUNCH(k_slot_write_L64, dim3(np / 4, nchains), dim3(256), 0, s, A, S, slots, mode,
                        np, live);
 }
 
@@ -422,5 +436,104 @@ __global__ __launch_bounds__(256) void k_export(Export e) {
 void launch_export(const Export& e, hipStream_t s) {
     const int tot = e.words[0] + e.words[1] + e.words[2] + e.words[3];
     if (tot <= 0) return;
-    hipLaunchKernelGGL(k_export, dim3((tot + 255) / 256), dim3(256), 0, s, e);
+    APM_LAUNCH(k_export, dim3((tot + 255) / 256), dim3(256), 0, s, e);
+}
+
+// ------------------------------------------------------------------------------------ the guard
+// DESIGN.md §11. Identities between independently computed parts of an IS theta-call; a chain
+// that breaks one beyond the rounding of its precisions fails with APM_STATUS_GUARD instead of
+// returning its value. G[k * B + b]: k = 0: 1/2 log|B| of the last Newton factor, summed after
+// the Newton loop (the factor the posterior's M = I + L_K^T W L_K shares its eigenvalues with,
+// W being the last iteration's); k = 1: 1/2 log|K| after chol(K); k = 2..4: the residuals.
+__global__ __launch_bounds__(64) void k_guard_save(const double* __restrict__ ldet,
+                                                   int64_t lstride, int off, int nb, double* G,
+                                                   int B, int k, Live live, int nchains) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= nchains || live.status[b] != 0) return;  // (converged chains are inactive here)
+    double s = 0.0;  // (the order of k_slot_write_vec's sum)
+    for (int q = 0; q < nb; ++q) s += ldet[b * lstride + off + q];
+    G[(int64_t)k * B + b] = s;
+}
+
+void launch_guard_save(const double* ldet, int64_t lstride, int off, int nb, double* G, int B,
+                       int k, Live live, int nchains, hipStream_t s) {
+    APM_LAUNCH(k_guard_save, dim3((nchains + 63) / 64), dim3(64), 0, s, ldet, lstride, off, nb, G,
+               B, k, live, nchains);
+}
+
+// r1 = |G0 - 1/2 log|M||, r2 = | |g|^2 - f_post^T z | / max(1, |f_post^T z|) (g = chol(C)^-1
+// f_post from L' and L_K, v.Kb; z = a + W f_post from the Newton vectors, in the slot), r3 =
+// |sum log diag(C_chol) - (G1 - 1/2 log|M|)| (C_chol = L_K U^-T: its diagonal is L_K,ii / U_ii;
+// from the fp32 slot; skipped for a chain whose bottom block is recomputed in fp64, bit 1 of
+// chain_wide). 1/2 log|M| is the ldet sum the slot's cst was formed with.
+__global__ __launch_bounds__(256) void k_guard_check(const double* __restrict__ ldet,
+                                                     int64_t lstride, int nb, const double* gvec,
+                                                     int64_t gstride, SlotSet S,
+                                                     const int64_t* __restrict__ slots, double* G,
+                                                     int B, double t1, double t2, double t3,
+                                                     double t4, const double* rowe,
+                                                     const double* fvec, int fail_code,
+                                                     Live live) {
+    const int b = blockIdx.x;
+    if (live.status[b] != 0 || live.active[b] == 0) return;
+    __shared__ double red[4];
+    const int64_t np = (int64_t)nb * 64;
+    const int64_t sl = slots[b];
+    const int64_t so = sl * S.vstride;
+    const float* L = S.L + sl * S.lstride;
+    double gg = 0.0, fz = 0.0, lc = 0.0, em = 0.0, fm = 0.0;
+    for (int64_t i = threadIdx.x; i < np; i += 256) {
+        const double g = gvec[b * gstride + i];
+        gg += g * g;
+        fz += S.fpost64[so + i] * S.z64[so + i];
+        lc += log((double)L[i * np + i]);
+        em = fmax(em, fabs(rowe[b * np + i]));  // (a NaN row makes em NaN: fmax drops it, so
+        if (rowe[b * np + i] != rowe[b * np + i]) em = INFINITY;  // it is caught here)
+        fm = fmax(fm, fabs(fvec[b * gstride + i]));
+    }
+    gg = block_sum_d(gg, red);
+    __syncthreads();
+    fz = block_sum_d(fz, red);
+    __syncthreads();
+    lc = block_sum_d(lc, red);
+    __syncthreads();
+    em = block_max_d(em, red);
+    __syncthreads();
+    fm = block_max_d(fm, red);
+    if (threadIdx.x == 0) {
+        double ldm = 0.0;
+        for (int q = 0; q < nb; ++q) ldm += ldet[b * lstride + q];
+        const double r1 = fabs(G[b] - ldm);
+        const double r2 = fabs(gg - fz) / fmax(1.0, fabs(fz));
+        const bool fp64_bottom = S.chain_wide[b] & 2;  // (recomputed in fp64 after this)
+        const double r3 = fp64_bottom ? 0.0 : fabs(lc - (G[B + b] - ldm));
+        const double r4 = fp64_bottom ? 0.0 : em / fmax(1.0, fm);
+        G[2 * (int64_t)B + b] = r1;
+        G[3 * (int64_t)B + b] = r2;
+        G[4 * (int64_t)B + b] = r3;
+        G[5 * (int64_t)B + b] = r4;
+        // (!(r <= t): a NaN residual fails as well)
+        if (!(r1 <= t1) || !(r2 <= t2) || !(r3 <= t3) || !(r4 <= t4))
+            live.status[b] = fail_code;
+    }
+}
+
+void launch_guard_check(const double* ldet, int64_t lstride, int nb, const double* gvec,
+                        int64_t gstride, SlotSet S, const int64_t* slots, double* G, int B,
+                        double t1, double t2, double t3, double t4, const double* rowe,
+                        const double* fvec, int fail_code, Live live, int nchains,
+                        hipStream_t s) {
+    APM_LAUNCH(k_guard_check, dim3(nchains), dim3(256), 0, s, ldet, lstride, nb, gvec, gstride, S,
+               slots, G, B, t1, t2, t3, t4, rowe, fvec, fail_code, live);
+}
+
+// APM_SKEW (tests only): a kernel that only waits, `us` microseconds of the 100 MHz constant
+// clock (s_memrealtime), one wave
+__global__ __launch_bounds__(64) void k_delay(long long ticks) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void launch_delay(int us, hipStream_t s) {
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (long long)us * 100);
 }

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_set_rhs(MatB A, int64_t row0, int ncols
 
 void launch_set_rhs(MatB A, int64_t row0, int ncols, const double* vec, int64_t vstride,
                     Live live, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_set_rhs, dim3((ncols + 63) / 64, nchains), dim3(256), 0, s, A, row0, ncols,
+    APM_LAUNCH(k_set_rhs, dim3((ncols + 63) / 64, nchains), dim3(256), 0, s, A, row0, ncols,
                        vec, vstride, live);
 }
 
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_get_row(MatB A, int64_t row, int n, dou
 
 void launch_get_row(MatB A, int64_t row, int n, double* out, int64_t ostride, Live live,
                     int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_get_row, dim3((n + 255) / 256, nchains), dim3(256), 0, s, A, row, n, out,
+    APM_LAUNCH(k_get_row, dim3((n + 255) / 256, nchains), dim3(256), 0, s, A, row, n, out,
                        ostride, live);
 }
 
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_form_y2_rev(MatB L, MatB dst, int64_t d
 void launch_form_y2_rev(MatB L, MatB dst, int64_t dcol0, const double* Ws, int64_t vstride,
                         int np, Live live, int nchains, hipStream_t s, bool zero_all) {
     const int nb = np / 64;
-    hipLaunchKernelGGL(k_form_y2_rev, dim3(nb * ((nb + 1) / 2), nchains), dim3(256), 0, s, L, dst,
+    APM_LAUNCH(k_form_y2_rev, dim3(nb * ((nb + 1) / 2), nchains), dim3(256), 0, s, L, dst,
                        dcol0, Ws, vstride, nb, live, (int)zero_all);
 }
 
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_identity_lower(MatB M, Live live) {
 
 void launch_identity_lower(MatB M, int np, Live live, int nchains, hipStream_t s) {
     const int nb = np / 64;
-    hipLaunchKernelGGL(k_identity_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, M, live);
+    APM_LAUNCH(k_identity_lower, dim3(nb * (nb + 1) / 2, nchains), dim3(256), 0, s, M, live);
 }
 
 // g = J L'^T J h: g[np-1-c] = sum_{r >= c} L'[r][c] h[np-1-r] (REV), or out[c] = sum_{r >= c}
@@ -242,14 +242,14 @@ void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t v
     const int nb = np / 64;
     const dim3 gp(nb * (nb + 1) / 2, nchains), gr((np + 255) / 256, nchains);
     if (rev) {
-        hipLaunchKernelGGL(k_trmv_part<true>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
+        APM_LAUNCH(k_trmv_part<true>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
                            nb, live);
-        hipLaunchKernelGGL(k_trmv_reduce<true>, gr, dim3(256), 0, s, part, pstride, nb, out,
+        APM_LAUNCH(k_trmv_reduce<true>, gr, dim3(256), 0, s, part, pstride, nb, out,
                            vstride, live);
     } else {
-        hipLaunchKernelGGL(k_trmv_part<false>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
+        APM_LAUNCH(k_trmv_part<false>, gp, dim3(256), 0, s, L, x, vstride, part, pstride,
                            nb, live);
-        hipLaunchKernelGGL(k_trmv_reduce<false>, gr, dim3(256), 0, s, part, pstride, nb, out,
+        APM_LAUNCH(k_trmv_reduce<false>, gr, dim3(256), 0, s, part, pstride, nb, out,
                            vstride, live);
     }
 }
@@ -307,7 +307,7 @@ void launch_post32_convert(MatB A, MatF S32, const double* D64, int64_t d64strid
     const int nc = k1 - k0, T = (nb - k0) * nc;
     const int grid = T + nc + (bottom ? nb * nb : 0);
     if (grid <= 0) return;
-    hipLaunchKernelGGL(k_post32_convert, dim3(grid, nchains), dim3(256), 0, s, A, S32, D64,
+    APM_LAUNCH(k_post32_convert, dim3(grid, nchains), dim3(256), 0, s, A, S32, D64,
                        d64stride, D32, d32stride, nb, outer, k0, k1, live);
 }
 
@@ -317,6 +317,6 @@ __global__ void k_merge_status(int* status, const int* other, int code, int ncha
 }
 
 void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s) {
-    hipLaunchKernelGGL(k_merge_status, dim3((nchains + 255) / 256), dim3(256), 0, s, status, other,
+    APM_LAUNCH(k_merge_status, dim3((nchains + 255) / 256), dim3(256), 0, s, status, other,
                        code, nchains);
 }

@@ -28,7 +28,7 @@ void launch_u_convert(const double* U64, int64_t ldu, int n, int S, UPool P, int
                       hipStream_t s) {
     const int np = (int)(P.stride / P.sp);
     const int64_t tot = (int64_t)np * P.sp;
-    hipLaunchKernelGGL(k_u_convert, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, U64, ldu,
+    APM_LAUNCH(k_u_convert, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, U64, ldu,
                        n, S, P.base + ubuf * P.stride, P.base32 + ubuf * P.stride, P.sp, np);
 }
 
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_philox_test(const uint32_t* __restrict_
 }
 
 void launch_philox_test(const uint32_t* in, uint32_t* out, int64_t n, hipStream_t s) {
-    hipLaunchKernelGGL(k_philox_test, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out,
+    APM_LAUNCH(k_philox_test, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out,
                        n);
 }
 
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_u_normal(UPool P, const int64_t* __rest
 void launch_u_normal(UPool P, const int64_t* ubufs, const uint64_t* seeds,
                      const uint64_t* counters, int n, int S, int nchains, hipStream_t s) {
     const int64_t groups = ((int64_t)n * S + 3) / 4;
-    hipLaunchKernelGGL(k_u_normal, dim3((unsigned)((groups + 255) / 256), nchains), dim3(256), 0, s,
+    APM_LAUNCH(k_u_normal, dim3((unsigned)((groups + 255) / 256), nchains), dim3(256), 0, s,
                        P, ubufs, seeds, counters, n, S);
 }
 
@@ -125,7 +125,7 @@ void launch_u_combine(UPool P, const int64_t* dst, const int64_t* a, const int64
     (void)n;
     (void)S;
     const int64_t tot = P.stride;  // padded entries are 0 in both inputs, stay 0
-    hipLaunchKernelGGL(k_u_combine, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0, s,
+    APM_LAUNCH(k_u_combine, dim3((unsigned)((tot + 255) / 256), nchains), dim3(256), 0, s,
                        P, dst, a, b, ca, cb, tot);
 }
 
@@ -350,10 +350,10 @@ void launch_ugemm(SlotSet S, const int64_t* slots, UPool P, const int64_t* ubufs
                   const int* status, int nchains, bool wide, hipStream_t s) {
     const int nb = np / 64, nsb = P.sp / 64;
     const long total = (long)nb * nsb * nchains;
-    hipLaunchKernelGGL(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
+    APM_LAUNCH(k_ugemm, dim3((unsigned)total), dim3(256), 0, s, S, slots, P, ubufs, y, n,
                        np, partial, pstride, status, nsb, nchains);
     if (wide)
-        hipLaunchKernelGGL(k_ugemm64, dim3((unsigned)(nb * nsb), nchains), dim3(256), 0, s, S,
+        APM_LAUNCH(k_ugemm64, dim3((unsigned)(nb * nsb), nchains), dim3(256), 0, s, S,
                            slots, P, ubufs, y, n, np, partial, pstride, status, nsb);
 }
 
@@ -396,6 +396,6 @@ __global__ __launch_bounds__(256) void k_lme(const double* __restrict__ partial,
 void launch_lme(const double* partial, int64_t pstride, int nb, int S, int sp, SlotSet Sl,
                 const int64_t* slots, double* out, const int* status, int nchains,
                 hipStream_t s) {
-    hipLaunchKernelGGL(k_lme, dim3(nchains), dim3(256), 0, s, partial, pstride, nb, S, sp, Sl,
+    APM_LAUNCH(k_lme, dim3(nchains), dim3(256), 0, s, partial, pstride, nb, S, sp, Sl,
                        slots, out, status);
 }

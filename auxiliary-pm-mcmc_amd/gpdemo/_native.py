@@ -18,9 +18,11 @@ KERNEL_ISO, KERNEL_ARD, KERNEL_PRECOMPUTED = 0, 1, 2
 EST_IS, EST_PRIORMC, EST_LAPLACE = 0, 1, 2
 APM_SUCCESS, APM_E_INVALID, APM_E_HIP, APM_E_NOMEM = 0, -1, -2, -3
 STATUS_OK, STATUS_CHOL_K, STATUS_CHOL_B, STATUS_CHOL_C, STATUS_MAXITER = 0, 1, 2, 3, 4
+STATUS_GUARD = 5
 PROF_GRAM, PROF_CHOL_UPDATE, PROF_UGEMM, PROF_CHOL_UPDATE32, PROF_STATS = 0, 1, 2, 3, 4
 PROF_CHOL_UPDATE32_OUTER, PROF_CHOL_UPDATE_OUTER, PROF_DF_TIMEOUTS = 5, 6, 7
-PROF_POST32_OUTER, PROF_POST64_RERUNS, PROF_TRSV_TIMEOUTS, PROF_NKINDS = 8, 9, 10, 11
+PROF_POST32_OUTER, PROF_POST64_RERUNS, PROF_TRSV_TIMEOUTS = 8, 9, 10
+PROF_ICM_CHECKS, PROF_GUARD, PROF_NKINDS = 11, 12, 13
 
 
 class NativeUnavailableError(RuntimeError):
@@ -64,6 +66,7 @@ _SIGS = {
     'apm_prof_enable': (_i, [_p, _i]),
     'apm_prof_marker': (_i, [_p, _i]),
     'apm_prof_read': (_i, [_p, _i, _p, _p, _p, _i]),
+    'apm_guard_read': (_i, [_p, _i64, _p]),
     'apm_selftest_tile': (_i, [_i, _p, _p, _p]),
     'apm_selftest_philox': (_i, [_i, _i64, _p, _p]),
 }
@@ -338,6 +341,12 @@ class Context(object):
         _check(self.lib.apm_slot_read(self._h, int(slot), _ptr(L), self.n, _ptr(f), _ptr(g),
                                       _ptr(c)), self._h)
         return L, f, g, float(c[0])
+
+    def guard_read(self, count):
+        """(count, 4) residuals r1..r4 of the last IS theta-call's guard (include/apm.h)."""
+        r = np.zeros((int(count), 4))
+        _check(self.lib.apm_guard_read(self._h, int(count), _ptr(r)), self._h)
+        return r
 
     # --- profiling
     def prof_enable(self, on=True):

@@ -17,13 +17,19 @@ from .latent_posterior_approximations import MaximumIterationsExceededError
 
 __all__ = ['LogMarginalLikelihoodLaplaceEstimator', 'InvalidCovarianceMatrixError',
            'LogMarginalLikelihoodApproxPosteriorISEstimator',
-           'LogMarginalLikelihoodPriorMCEstimator', 'DeviceCache']
+           'LogMarginalLikelihoodPriorMCEstimator', 'DeviceCache', 'DeviceInvariantError']
 
 _UBUF = 0  # single-chain estimators upload each call's draws into this device buffer
 
 
 class InvalidCovarianceMatrixError(Exception):
     """Raised when the posterior approximation's covariance is not positive definite."""
+
+
+class DeviceInvariantError(RuntimeError):
+    """A device-side invariant of the theta-call failed (APM_STATUS_GUARD): the
+    estimate is withheld rather than returned. No reference counterpart (the reference has no
+    device); a sampler treats it like any other failed estimator call."""
 
 
 class DeviceCache(object):
@@ -103,6 +109,9 @@ def _raise_for_status(status, ctx, n_iter_cap=1000):
         raise InvalidCovarianceMatrixError(
             'Posterior covariance matrix not PSD: sum of negative eigenvalues nan '
             '(Cholesky of C failed on the device)')
+    if status == _native.STATUS_GUARD:
+        raise DeviceInvariantError('a device-side invariant of the theta-call failed '
+                                   '(apm_guard_read gives the residuals)')
     if status == _native.STATUS_MAXITER:
         raise MaximumIterationsExceededError('Failed to converge in {0} iterations'
                                              .format(n_iter_cap))

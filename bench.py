@@ -366,12 +366,24 @@ PARITY_U_SEED = 5         # U1, U2: the first two (N, S) normal draws of RandomS
 REF_FIXTURE = os.path.join(REPO, 'tests', 'golden', 'config2_ref.npz')
 
 
+# the headline's regime in the parity block: one of the long-chain record's stationary chain
+# states (tests/golden/stationary_thetas.npy row 45, log sigma 3.11: 10 cubic ops per theta-call
+# in the reference), row 4 of the reference fixture (make_golden_fullsize.py config2_stationary)
+PARITY_STATIONARY_ROW, PARITY_STATIONARY_FIXTURE_ROW = 45, 4
+
+
 def parity_inputs(n, d, s):
+    """The parity thetas, their rows in the reference fixture, and the draws U1, U2."""
     base = np.log(np.sqrt(d))
-    thetas = np.stack([np.r_[0.0, np.full(d, base)],          # theta* (cpu_baseline's theta)
-                       np.r_[1.0, np.full(d, base + 2.0)]])   # long length-scale
+    thetas = [np.r_[0.0, np.full(d, base)],          # theta* (cpu_baseline's theta)
+              np.r_[1.0, np.full(d, base + 2.0)]]    # long length-scale
+    rows = [0, 1]
+    st = np.load(os.path.join(REPO, 'tests', 'golden', 'stationary_thetas.npy'))
+    if st.shape[1] == d + 1:  # (the bench's ARD dimension)
+        thetas.append(st[PARITY_STATIONARY_ROW].astype(np.float64))
+        rows.append(PARITY_STATIONARY_FIXTURE_ROW)
     rng = np.random.RandomState(PARITY_U_SEED)
-    return thetas, rng.normal(size=(n, s)), rng.normal(size=(n, s))
+    return np.stack(thetas), rows, rng.normal(size=(n, s)), rng.normal(size=(n, s))
 
 
 def device_counters(ctx):
@@ -427,7 +439,7 @@ def reference_fixture(X, y, n, d, s, seed):
     return z, 'ok'
 
 
-def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
+def parity_check(dist, X, y, a, thetas, fix_rows, U1, U2, oracle_first):
     """GPU (every rank) vs oracle (rank 0, broadcast) and vs the reference fixture."""
     import apm_oracle as orc
     B, n = thetas.shape[0], X.shape[0]
@@ -488,7 +500,9 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
             'device_counters': {k: (None if np.isnan(v) else int(v))
                                 for k, v in zip(COUNTER_NAMES, ctr)}})
     out = {'thetas': ['theta* (log sigma 0, log tau_k log sqrt(D))',
-                      'long length-scale (log sigma 1, log tau_k log sqrt(D) + 2)'],
+                      'long length-scale (log sigma 1, log tau_k log sqrt(D) + 2)',
+                      'stationary chain state (tests/golden/stationary_thetas.npy row {0}, log '
+                      'sigma {1:.2f})'.format(PARITY_STATIONARY_ROW, thetas[-1][0])][:B],
            'draws': 'U1, U2 = first two (N, N_imp) normal draws of RandomState({0}); theta-call '
                     'on U1, cached u-call on U2'.format(PARITY_U_SEED),
            'checked_ranks': int(dist.world),
@@ -512,15 +526,20 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
     z, why = reference_fixture(X, y, a.n, a.d, a.n_imp, a.seed)
     ref = {'fixture': os.path.relpath(REF_FIXTURE, REPO), 'used': z is not None, 'why': why}
     if z is not None:
+        have = [r for r in fix_rows if r < z['thetas'].shape[0]]
+        if len(have) < B or not np.array_equal(z['thetas'][have], thetas):
+            z, why = None, 'fixture rows {0} hold other thetas'.format(fix_rows)
+    if z is not None:
         gv1 = allr[:, 5 * B:6 * B]
         gv2 = allr[:, 6 * B:7 * B]
-        r1, r2 = z['logf1'][:B], z['logf2'][:B]
-        rf = z['f_post'][:B]
+        r1, r2 = z['logf1'][fix_rows], z['logf2'][fix_rows]
+        rf = z['f_post'][fix_rows]
         ref.update({
             'reference_theta_call': r1.tolist(), 'reference_u_call': r2.tolist(),
             'd_theta_call': float(np.abs(gv1 - r1).max()),
             'd_u_call': float(np.abs(gv2 - r2).max()),
-            'n_cubic_ops_equal': bool((orc_vals[:, 2] == z['n_cubic_ops'][:B]).all() and
+            'fixture_rows': list(fix_rows),
+            'n_cubic_ops_equal': bool((orc_vals[:, 2] == z['n_cubic_ops'][fix_rows]).all() and
                                       (dops == 0).all()),
             'oracle_minus_reference': {
                 'theta_call': float(np.abs(orc_vals[:, 0] - r1).max()),
@@ -530,6 +549,8 @@ def parity_check(dist, X, y, a, thetas, U1, U2, oracle_first):
         # the GPU's f_post vs the reference's: oracle's (checked above) within its own pin
         ok = ok and ref['d_theta_call'] <= PARITY_TOL_NATS and \
             ref['d_u_call'] <= PARITY_TOL_NATS and ref['n_cubic_ops_equal']
+    ref['used'] = z is not None
+    ref['why'] = why
     out['vs_reference'] = ref
     out['pass'] = bool(ok)
     return out
@@ -952,7 +973,7 @@ def main():
 
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     cpu, first = None, None
-    thetas_par, U1, U2 = parity_inputs(a.n, a.d, a.n_imp)
+    thetas_par, fix_rows, U1, U2 = parity_inputs(a.n, a.d, a.n_imp)
     if a.cpu_baseline and dist.rank == 0:
         try:  # (rank 0 alone: a failure here must not strand the others in the parity check)
             cpu, first = cpu_baseline(X, y, a.n_imp, thetas_par[0], n_th, n_u, a.cpu_budget,
@@ -960,7 +981,7 @@ def main():
             cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
         except Exception as e:  # noqa: BLE001
             cpu, first = {'error': repr(e)}, None
-    parity = parity_check(dist, X, y, a, thetas_par, U1, U2, first) if a.parity else None
+    parity = parity_check(dist, X, y, a, thetas_par, fix_rows, U1, U2, first) if a.parity else None
 
     # per-rank record: device, chains, transitions, elapsed, failures and the device counters of
     # the timed run (8 distinct devices, even load, no silent spin exits)
@@ -1045,6 +1066,23 @@ def main():
             .format(lr['source'], lr['ess_per_transition_min_component'], value, lr['rhat_max'],
                     'converged' if lr['converged_rhat_below_1p1'] else
                     'NOT converged: R-hat > 1.1'))
+    # the paper's efficiency column N_eff / N_cub.op (Analyse results.ipynb: effectiveSize over
+    # the run's n_cubic_ops / 1000, n_cubic_ops counted as estimators.py:81,217,322 - an IS
+    # theta-call costs its Newton iterations + 3, a cached u-call none): ESS per transition ÷
+    # cubic ops per transition x 1000, from the long-chain record's ESS per transition and this
+    # run's theta-calls per transition x cubic ops per theta-call (per chain)
+    cops_call = line['cubic_ops_per_theta_call']['mean_of_batch_mean']
+    if lr is not None and cops_call and n_th:
+        cop_tr = n_th * cops_call
+        eptm = lr.get('ess_per_transition_mean_component')
+        line['ess_per_kcop'] = {
+            'min_component': 1e3 * lr['ess_per_transition_min_component'] / cop_tr,
+            'mean_component': 1e3 * eptm / cop_tr if eptm is not None else None,
+            'cubic_ops_per_transition': cop_tr,
+            'source': 'long-chain record {0} (ESS per transition; R-hat max {1:.3f}) / (this '
+                      'run\'s theta_calls_per_transition {2:.3f} x cubic_ops_per_theta_call '
+                      'mean_of_batch_mean {3:.3f}) x 1000; Analyse results.ipynb '
+                      'N_eff/N_cub.op'.format(lr['source'], lr['rhat_max'], n_th, cops_call)}
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     ok = parity is None or parity['pass']

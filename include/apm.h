@@ -45,6 +45,9 @@ extern "C" {
 #define APM_STATUS_CHOL_B 2   /* chol(B) not PD        -> numpy.linalg.LinAlgError (lpa.py:92) */
 #define APM_STATUS_CHOL_C 3   /* chol(C) not PD        -> InvalidCovarianceMatrixError (estimators.py:208-215) */
 #define APM_STATUS_MAXITER 4  /* Newton not converged  -> MaximumIterationsExceededError (lpa.py:100-102) */
+#define APM_STATUS_GUARD 5    /* a device-side invariant of the theta-call failed (apm_guard_read;
+                                 DESIGN.md §11): the value is withheld -> DeviceInvariantError
+                                 (no reference counterpart: the reference has no device) */
 
 /* covariance kernels */
 #define APM_KERNEL_ISO 0         /* kernels.pyx:12-49, theta = (log sigma, log tau) */
@@ -141,7 +144,10 @@ int apm_laplace(int device, const double *K, int64_t n, int64_t ldk, const doubl
 #define APM_PROF_TRSV_TIMEOUTS 10 /* not a kernel: launches = bounded-spin timeouts of the Newton
                                     solves' multi-workgroup TRSV (each fails its chain, which the
                                     Newton loop reruns in fp64) */
-#define APM_PROF_NKINDS 11
+#define APM_PROF_ICM_CHECKS 11 /* not a kernel: launches = chains whose chol(C) was also formed the
+                                 reference's way (the InvalidCovarianceMatrixError check) */
+#define APM_PROF_GUARD 12 /* not a kernel: launches = chains failed by the guard (APM_STATUS_GUARD) */
+#define APM_PROF_NKINDS 13
 /* on = 0 off; 1 the roofline kinds (GRAM, UGEMM and the two *_OUTER kinds: one event pair per
  * launch of those kernels only, so that the timing adds little to a timed region); 2 every kind
  * (CHOL_UPDATE / CHOL_UPDATE32 add an event pair around every in-panel update launch) */
@@ -154,6 +160,15 @@ int apm_prof_read(apm_ctx *ctx, int kind, double *total_ms, int64_t *launches, d
 /* launches the empty kernel k_apm_marker<id> (id 0..3) on the context stream: brackets a region
  * in a rocprofv3 kernel trace (tools/prof_window.py); no reference counterpart */
 int apm_prof_marker(apm_ctx *ctx, int id);
+
+/* The guard of the last IS theta-call: per chain i < count, r[4i..4i+3] =
+ * |1/2 log|B| of the last Newton factor - 1/2 log|M| of the posterior factor| (the same
+ * eigenvalues), | |g|^2 - f_post^T z | / max(1, |f_post^T z|) (g = chol(C)^-1 f_post from the
+ * posterior factors, z = a + W f_post from the Newton vectors), |sum log diag chol(C) -
+ * (1/2 log|K| - 1/2 log|M|)| (C_chol's diagonal from the slot) and max_r |(C_chol g)_r -
+ * f_post_r| / max(1, max |f_post|) (every row of the slot's fp32 factor). A chain past a bound
+ * fails with APM_STATUS_GUARD. */
+int apm_guard_read(apm_ctx *ctx, int64_t count, double *r);
 
 /* ---- self-test ------------------------------------------------------------------------------- */
 /* C = C + A * B^T for 64x64 row-major fp64 host matrices through the f64 MFMA tile routine that

@@ -58,12 +58,16 @@ def test_long_chain_record_and_provenance():
 
 def test_parity_inputs_match_reference_fixture():
     """The bench's parity thetas and draws are the ones tests/golden/config2_ref.npz holds the
-    reference's outputs for (so that the bench can compare against the reference itself)."""
+    reference's outputs for (so that the bench can compare against the reference itself),
+    including one stationary chain state of the headline's regime."""
     bench = _bench()
     from conftest import golden
     z = golden('config2_ref')
-    th, U1, U2 = bench.parity_inputs(int(z['n']), int(z['d']), int(z['s']))
-    np.testing.assert_array_equal(th, z['thetas'][:2])
+    th, rows, U1, U2 = bench.parity_inputs(int(z['n']), int(z['d']), int(z['s']))
+    assert len(rows) == 3 and th.shape[0] == 3
+    np.testing.assert_array_equal(th, z['thetas'][rows])
+    assert th[2, 0] > 3.0  # (log sigma of the stationary regime)
+    assert int(z['status'][rows].max()) == 0
     rng = np.random.RandomState(int(z['u_seed']))
     np.testing.assert_array_equal(U1, rng.normal(size=U1.shape))
     np.testing.assert_array_equal(U2, rng.normal(size=U2.shape))

@@ -197,18 +197,30 @@ def test_config2_stationary_states_match_fp64_newton(nat, monkeypatch):
 
 def test_config2_reference_route_check_passes_everywhere(nat, monkeypatch):
     """The reference-route check of chol(C) (capi.cpp icm_check) forced on
-    every chain (APM_ICM_Q huge) at configs[2]'s four thetas, sigma = e^18.5 included: C =
-    K - V^T V of the last Newton iteration factors on every chain (status 0, as in the
-    reference, which returned values there) and the estimates are bitwise those of the default
-    call (the check writes nothing the estimate reads)."""
+    every chain (APM_ICM_Q=1: trace(C) < n K_ii holds for every chain, C being below K) at
+    configs[2]'s four thetas, sigma = e^18.5 included: C = K - V^T V of the last Newton
+    iteration factors on every chain (status 0, as in the reference, which returned values
+    there), the check ran on all of them (APM_PROF_ICM_CHECKS), and the estimates are bitwise
+    those of the default call (the check writes nothing the estimate reads)."""
     from gpdemo.utils import synthetic_gp_data
     z = golden('config2_ref')
     X, y = synthetic_gp_data(int(z['n']), int(z['d']), int(z['data_seed']))
-    th = z['thetas'].astype(np.float64)
+    th = z['thetas'][:4].astype(np.float64)
     U = np.random.RandomState(int(z['u_seed'])).normal(size=(int(z['n']), int(z['s'])))
     ref = _run(nat, X, y, th, int(z['s']), U, monkeypatch)
-    o, st, nops, o2, f = _run(nat, X, y, th, int(z['s']), U, monkeypatch, APM_ICM_Q='1e300')
-    assert (ref[1] == 0).all() and (st == 0).all()
+    monkeypatch.setenv('APM_ICM_Q', '1')
+    B = th.shape[0]
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, int(z['s']), max_batch=B, n_slots=B, n_ubufs=1)
+    monkeypatch.delenv('APM_ICM_Q')
+    try:
+        ctx.u_upload(0, U)
+        o, st, nops = ctx.theta_eval(nat.EST_IS, th, [0] * B, list(range(B)))
+        checked = ctx.prof_read(nat.PROF_ICM_CHECKS)[1]
+        o2, st2 = ctx.u_eval(list(range(B)), [0] * B)
+    finally:
+        ctx.close()
+    assert checked == B, checked
+    assert (ref[1] == 0).all() and (st == 0).all() and (st2 == 0).all()
     np.testing.assert_array_equal(o, ref[0])
     np.testing.assert_array_equal(o2, ref[3])
     np.testing.assert_array_equal(nops, ref[2])

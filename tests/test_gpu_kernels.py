@@ -377,69 +377,72 @@ def test_fp16x3_updates_match_fp32_operands(nat, monkeypatch):
         assert ob1[b] == o1[b]
 
 
-@pytest.mark.parametrize('n', [2048, 1700])
-def test_update_operand_planes_bitwise(nat, monkeypatch, n):
-    """The Newton factorisation's trailing updates stage fp16x3 operand planes that the dataflow
-    panel kernel writes (chol32.hip Planes16; the far updates on 256x256 quad tiles,
-    k_chol_update32_q256) instead of splitting fp32 operands while staging them (APM_PLANES=0),
-    or run on the 128-row kernel only (APM_Q256=0): the same split of the same values and the
-    same MFMA sequence per tile, so outputs, modes and iteration counts are bitwise equal.
-    n = 1700: ragged quad tiles (row and column masks). With a chain at theta_0 = 19.5 in the
-    batch (fp32 operands) the quad path falls back to the 128-row kernel for the whole call,
-    again bitwise."""
+def _run_is_stats(nat, X, y, thetas, ns, monkeypatch, **env):
+    """_run_is plus the context's fp64 Newton-rerun count (APM_PROF_STATS launches)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    B = len(thetas)
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, ns.shape[1], max_batch=B, n_slots=B, n_ubufs=1)
+    for k in env:
+        monkeypatch.delenv(k)
+    ctx.u_upload(0, ns)
+    ctx.prof_read(nat.PROF_STATS, reset=True)
+    out, st, nops = ctx.theta_eval(nat.EST_IS, thetas, ubufs=[0] * B, slots=list(range(B)))
+    reruns = ctx.prof_read(nat.PROF_STATS)[1]
+    fs = [ctx.slot_read(b)[1] for b in range(B)]
+    ctx.close()
+    return out, st, nops, fs, reruns
+
+
+@pytest.mark.parametrize('n', [2048, 1700, 700])
+def test_panel_forms_are_batch_independent(nat, monkeypatch, n):
+    """The Newton factorisation takes, per chain, the explicit-inverse panel (chol32.hip
+    k_zinv_level32 + k_panel_inv_gemm32, chains with 1 + K_ii < 2^15), the dataflow walk with
+    fp16x3 operands (1 + K_ii >= 2^15, theta_0 < 19) or the walk with fp32 operands
+    (theta_0 >= 19); a batch whose chains all take the first runs compact dataflow launches and
+    the far updates on 256x256 quad tiles from the operand planes (k_chol_update32_q256),
+    otherwise every row walks or returns by its chain's flag and the far updates run on the
+    128-row super-tiles. Both forms perform the same split of the same values in the same MFMA
+    order, so a chain's mode and estimate are bitwise those it has in any other batch.
+    n = 1700: ragged quad tiles; n = 700: one full panel and a ragged last one (walked)."""
     X, y, thetas, ns = _mixed_case(n=n)
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_PLANES=0, APM_DFINV=0)
-    assert (s0 == 0).all()
-    for env in ({}, {'APM_Q256': 0}):
-        o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0, **env)
-        np.testing.assert_array_equal(s1, s0)
-        np.testing.assert_array_equal(n1, n0)
-        np.testing.assert_array_equal(o1, o0)
-        for b in range(len(thetas)):
-            np.testing.assert_array_equal(f1[b], f0[b])
-    big = thetas.copy()
-    big[2, 0] = 19.5
-    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_PLANES=0, APM_DFINV=0)
-    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch, APM_DFINV=0)
-    np.testing.assert_array_equal(sb1, sb0)
-    np.testing.assert_array_equal(nb1, nb0)
-    np.testing.assert_array_equal(ob1, ob0)
-    for b in range(len(big)):
-        if sb0[b] == 0:  # (a failed chain's slot is not written)
-            np.testing.assert_array_equal(fb1[b], fb0[b])
+    o1, s1, n1, f1, r1 = _run_is_stats(nat, X, y, thetas, ns, monkeypatch)
+    assert (s1 == 0).all() and r1 == 0
+    for extra in (12.0, 19.5):  # a walking fp16x3 chain / an fp32-operand chain in the batch
+        big = np.vstack([thetas, thetas[1]])
+        big[-1, 0] = extra
+        ob, sb, nbs, fb, rb = _run_is_stats(nat, X, y, big, ns, monkeypatch)
+        np.testing.assert_array_equal(sb[:3], s1)
+        np.testing.assert_array_equal(nbs[:3], n1)
+        for b in range(3):
+            np.testing.assert_array_equal(fb[b], f1[b])
+            assert ob[b] == o1[b], (extra, b, ob[b], o1[b])
+        if extra == 12.0:  # the walking chain is bitwise its value alone
+            oa, sa, na, fa, ra = _run_is_stats(nat, X, y, big[-1:], ns, monkeypatch)
+            assert sa[0] == sb[-1] and na[0] == nbs[-1]
+            if sa[0] == 0:
+                np.testing.assert_array_equal(fa[0], fb[-1])
+                assert oa[0] == ob[-1]
 
 
 @pytest.mark.parametrize('n', [2048, 700])
-def test_explicit_inverse_panels_match_walk(nat, monkeypatch, n):
-    """The explicit-inverse panels of the Newton factorisation (default; chol32.hip
-    k_panel_zt32 + k_panel_inv_gemm32: Z = inv(L_D) of each 512x512 diagonal block, then one
-    fp16x3 GEMM X_i = A_i Z^T per row tile below it) against the dataflow walk (APM_DFINV=0):
-    the rounding of the factor differs (the product with inv(L_D) amplifies its 22-bit fp16x3
-    operands by cond(L_D), where the walk's TRSM by the 64x64 inverses is fp32), the fp64
-    refinement makes the Newton modes agree to 1e-8 of their maximum (the f_post tolerance of
-    DESIGN.md §3.3; ~5e-9 measured at n = 2048) and the estimates to 1e-6, with the same
-    iteration counts. n = 700: one
-    full panel and a ragged last one (walked). A chain outside fp16's range walks its panels
-    (bitwise the walk) while the other chains of its batch keep the inverse panels (bitwise
-    their values without it): a chain's value does not depend on its batch."""
+def test_fp16x3_walk_range_against_fp64(nat, monkeypatch, n):
+    """Chains with theta_0 in 11 .. 18 (advisor r05: the explicit-inverse panel's fp16 split of
+    Schur-complement entries, bounded by 1 + K_ii, overflowed above theta_0 ~ 11, every call then
+    failing into the fp64 rerun): they walk their panels with fp16x3 operands (solved entries,
+    |L_ij| <= sqrt(1 + K_ii)), so no chain is rerun in fp64, and their modes and estimates match
+    the all-fp64 Newton iteration (APM_MIXED=0) within the f_post tolerance (1e-8 of the
+    maximum) and 1e-6 relative, with the same iteration counts."""
     X, y, thetas, ns = _mixed_case(n=n)
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0)
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch)
-    assert (s0 == 0).all() and (s1 == 0).all()
-    np.testing.assert_array_equal(n1, n0)
-    for b in range(len(thetas)):
-        np.testing.assert_allclose(f1[b], f0[b], rtol=0, atol=1e-8 * np.abs(f0[b]).max())
-        assert abs(o1[b] - o0[b]) <= 1e-6 * max(1.0, abs(o0[b])), (b, o1[b], o0[b])
-    big = thetas.copy()
-    big[2, 0] = 19.5
-    ob0, sb0, nb0, fb0 = _run_is(nat, X, y, big, ns, monkeypatch, APM_DFINV=0)
-    ob1, sb1, nb1, fb1 = _run_is(nat, X, y, big, ns, monkeypatch)
-    np.testing.assert_array_equal(sb1, sb0)
-    np.testing.assert_array_equal(nb1, nb0)
-    assert ob1[2] == ob0[2] or (sb0[2] != 0)
-    for b in (0, 1):
-        np.testing.assert_array_equal(fb1[b], f1[b])
-        assert ob1[b] == o1[b]
+    th = np.vstack([thetas[:2]] + [np.r_[t0, thetas[1, 1:]] for t0 in (11.0, 14.0, 17.0)])
+    o64, s64, n64, f64, _ = _run_is_stats(nat, X, y, th, ns, monkeypatch, APM_MIXED=0)
+    o32, s32, n32, f32, reruns = _run_is_stats(nat, X, y, th, ns, monkeypatch)
+    assert (s64 == 0).all() and (s32 == 0).all(), (s64, s32)
+    assert reruns == 0, 'a chain in the fp16x3 range was rerun in fp64'
+    np.testing.assert_array_equal(n32, n64)
+    for b in range(len(th)):
+        np.testing.assert_allclose(f32[b], f64[b], rtol=0, atol=1e-8 * np.abs(f64[b]).max())
+        assert abs(o32[b] - o64[b]) <= 1e-6 * max(1.0, abs(o64[b])), (b, o32[b], o64[b])
 
 
 def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
@@ -462,27 +465,18 @@ def _run_is_prof(nat, X, y, thetas, ns, monkeypatch, **env):
 
 @pytest.mark.parametrize('n', [700, 1100])
 def test_posterior_bottom_fp32_matches_fp64(nat, monkeypatch, n):
-    """The posterior factor's bottom block (L_K J) L'^-T in fp32 (default: beside the fp64
-    factorisation of J M J on the second stream, APM_POST32=1: after it; postcov.hip) against
-    the all-fp64 stacked factorisation (APM_POST32=0): Newton modes and log|B| untouched (bitwise
-    equal f_post and cst), chol(C) within fp32 accuracy of its maximum, estimates within 1e-4
-    nats (the fp32 TRSM moves log f by ~1e-9 x trace(C)). n = 1100: a ragged last outer panel.
-    Also the fp64 recomputation of the chains above the trace bound (APM_POST32_Q=0: all of them)
-    against the all-fp64 path: fp64 either way, to 1e-9 relative."""
+    """The posterior factor's bottom block (L_K J) L'^-T in fp32 beside the fp64 factorisation of
+    J M J on the second stream (postcov.hip) against its fp64 recomputation (APM_POST32_Q=0: the
+    trace bound above which a chain's bottom block is recomputed in fp64 from the intact fp64
+    rows, here every chain): Newton modes and log|B| untouched (bitwise equal f_post and cst),
+    chol(C) within fp32 accuracy of its maximum, estimates within 1e-4 nats (the fp32 TRSM moves
+    log f by ~1e-9 x trace(C)). n = 1100: a ragged last outer panel."""
     X, y, thetas, ns = _mixed_case(n=n)
-    o0, s0, n0, r0, k0, u0 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32=0)
+    o0, s0, n0, r0, k0, u0 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32_Q=0)
     o1, s1, n1, r1, k1, u1 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch)
-    o2, s2, n2, r2, k2, u2 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32_Q=0)
-    # the bottom block after the fp64 factorisation instead of beside it: the same kernels on the
-    # same operands, bitwise
-    o3, s3, n3, r3, k3, u3 = _run_is_prof(nat, X, y, thetas, ns, monkeypatch, APM_POST32=1)
-    np.testing.assert_array_equal(o3, o1)
-    np.testing.assert_array_equal(u3, u1)
-    for b in range(len(thetas)):
-        np.testing.assert_array_equal(r3[b][0], r1[b][0])
-    assert (s0 == 0).all() and (s1 == 0).all() and (s2 == 0).all()
+    assert (s0 == 0).all() and (s1 == 0).all()
     np.testing.assert_array_equal(n1, n0)
-    assert k0 == 0 and k2 == len(thetas)
+    assert k1 == 0 and k0 == len(thetas)
     for b in range(len(thetas)):
         L0, f0, g0, c0 = r0[b]
         L1, f1, g1, c1 = r1[b]
@@ -491,34 +485,6 @@ def test_posterior_bottom_fp32_matches_fp64(nat, monkeypatch, n):
         assert np.abs(L1 - L0).max() <= 1e-5 * np.abs(L0).max(), (b, np.abs(L1 - L0).max())
         assert abs(o1[b] - o0[b]) <= 1e-4, (b, o1[b], o0[b])
         assert abs(u1[b] - u0[b]) <= 1e-4, (b, u1[b], u0[b])
-        L2 = r2[b][0]
-        assert np.abs(L2 - L0).max() <= 1e-6 * np.abs(L0).max()
-        assert abs(o2[b] - o0[b]) <= 1e-9 * max(1.0, abs(o0[b])), (b, o2[b], o0[b])
-
-
-@pytest.mark.parametrize('n', [560, 1100])
-def test_dataflow_panel_matches_launch_sequence(nat, monkeypatch, n):
-    """The Newton factor's in-panel steps in two forms with the same operands and the same
-    accumulation order, so modes, estimates, statuses and iteration counts are bitwise equal - also
-    for a batch with a chain at an extreme theta (fp32 operands, possibly a failed fp32
-    factorisation and its fp64 rerun) next to ordinary ones: the per-column launch sequence
-    (APM_DF32=0) and the default, one dataflow launch per outer panel whose rows walk the panel's
-    columns (k_chol_panel_df32; the explicit-inverse panels off, APM_DFINV=0: they round
-    differently, test_explicit_inverse_panels_match_walk). n = 560: a last outer panel of one
-    column (its TRSM only), n = 1100: three outer panels, the last of two."""
-    X, y, thetas, ns = _mixed_case(n=n)
-    ext = thetas[0].copy()
-    ext[0] = 45.0
-    thetas = np.vstack([thetas, ext])
-    o0, s0, n0, f0 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DF32=0)
-    assert (s0[:3] == 0).all()
-    o1, s1, n1, f1 = _run_is(nat, X, y, thetas, ns, monkeypatch, APM_DFINV=0)
-    np.testing.assert_array_equal(s1, s0)
-    np.testing.assert_array_equal(n1, n0)
-    for b in range(len(thetas)):
-        if s0[b] == 0:
-            np.testing.assert_array_equal(f1[b], f0[b])
-            assert o1[b] == o0[b], (b, o1[b], o0[b])
 
 
 @pytest.mark.parametrize('tol', [0.0, 1e-7])
