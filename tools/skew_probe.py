@@ -20,7 +20,16 @@ def main():
     ap.add_argument('modes', nargs='+')
     ap.add_argument('--calls', type=int, default=2)
     ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--env', nargs='*', default=[], help='VAR=value for every context')
+    ap.add_argument('--pkg', default=None,
+                    help='import gpdemo from this directory instead (another build\'s binding; '
+                         'with APM_LIB naming its library)')
     a = ap.parse_args()
+    if a.pkg:
+        sys.path.insert(0, a.pkg)
+    for kv in a.env:
+        k, v = kv.split('=', 1)
+        os.environ[k] = v
     from gpdemo import _native
     from gpdemo import utils
     X, y = utils.synthetic_gp_data(4096, 32, 20151009)
@@ -40,7 +49,7 @@ def main():
             out, st, nops = ctx.theta_eval(_native.EST_IS, th, idx, idx)
             t1 = time.perf_counter()
             out2, st2 = ctx.u_eval(idx, idx)
-            g = ctx.guard_read(B)
+            g = ctx.guard_read(B) if hasattr(ctx, 'guard_read') else np.zeros((B, 4))
             if base is None:
                 base = (out.copy(), out2.copy())
             ok = st == 0
