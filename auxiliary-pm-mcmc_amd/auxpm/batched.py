@@ -170,18 +170,30 @@ class _BatchedChains(object):
         return self.theta.copy()
 
     # ------------------------------------------------------------------ checkpoint / resume
-    def checkpoint(self, store_u=False):
+    def checkpoint(self, store_u=None):
         """Chain state at a transition boundary as a dict of numpy arrays (``numpy.savez``-able,
         no pickles): theta, log f, log prior, failure flags, rejection counts, device counters,
         each chain's RandomState (MT19937 key and position, cached Gaussian) and the u history.
-        By default u itself (N x N_imp fp64 per chain) is not stored: ``restore`` rebuilds it on
-        the device from the history with the same kernels, bit for bit - a replay that grows
-        with the chain. ``store_u=True`` downloads u instead (fp64, exact: the device's fp32
-        mirror is the rounding of those values, so an upload restores both bit for bit) and
-        restarts the history at this snapshot, so restore time and u-log size stop growing;
-        every later checkpoint then carries u as well."""
+
+        Two forms, chosen by ``store_u``:
+        * compact (``False``; the default until a snapshot is taken): u itself (N x N_imp fp64 per
+          chain) is not stored; ``restore`` rebuilds it on the device from the Philox draws and
+          accepted moves since initialisation, bit for bit - a replay that grows with the chain.
+          No side effects.
+        * snapshot (``True``): u is downloaded (fp64, exact: the device's fp32 mirror is the
+          rounding of those values, so an upload restores both bit for bit) and the history
+          restarts at this snapshot, so restore time and u-log size stop growing. That restart is
+          a side effect on the sampler: the replay base is now this snapshot, which the compact
+          form cannot express, so after a snapshot ``store_u=None`` (the default) takes a
+          snapshot again and ``store_u=False`` raises ValueError.
+        """
         C = self.n_chains
-        if store_u or self.u_snapshot:
+        if store_u is None:
+            store_u = self.u_snapshot
+        if not store_u and self.u_snapshot:
+            raise ValueError('the u history restarts at the last u snapshot: a compact (replay) '
+                             'checkpoint cannot rebuild u from it; pass store_u=True or None')
+        if store_u:
             u = np.zeros((C, self.ctx.n, self.n_imp))
             for c in np.flatnonzero(~self.failed):
                 u[c] = self.ctx.u_download(self.ub_u[c])

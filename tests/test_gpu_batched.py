@@ -263,7 +263,9 @@ def test_run_async_finish_mode_ends_on_boundaries(gpu_available, tmp_path):
         assert c.restore({k: z[k] for k in z.files}) == 0.
     tc2, _ = c.run_async(2)
     np.testing.assert_array_equal(np.array(ta2), np.array(tc2))
-    assert 'u' in c.checkpoint()  # later checkpoints keep carrying u
+    assert 'u' in c.checkpoint()  # later checkpoints keep carrying u (store_u=None)
+    with pytest.raises(ValueError):  # a replay checkpoint cannot start from a snapshot
+        c.checkpoint(store_u=False)
 
 
 def test_batched_mi_seqslice_consistent_and_batch_invariant(gpu_available):

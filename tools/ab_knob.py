@@ -4,7 +4,7 @@ APM_* environment variable (read by apm_create), timed over --reps calls after o
 with the outputs compared against the first value's: max |d log f|, n_cubic_ops and status equal,
 and a per-phase kernel-time split from the library's profiling counters.
 
-    python tools/ab_knob.py APM_DFINV 0 1 [--reps 3] [--batch 64]
+    python tools/ab_knob.py APM_H3 0 1 [--reps 3] [--batch 64]
 """
 import argparse
 import hashlib
