@@ -129,7 +129,8 @@ void launch_panel_inv32(MatF A, int K, int nb, const float* Dinv, int64_t dstrid
 // tile i is zero in the tile columns < zrow - 1 - i (postcov.hip's fp32 bottom block)
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
                               FusedDiag<float> fd, Live live, int nchains, int hlim,
-                              const int* h3ok, hipStream_t s);
+                              const int* h3ok, hipStream_t s,
+                              Planes16 pl = Planes16{nullptr, 0, 0, 0});
 void launch_chol_update32(MatF A, int k0, int kc, const unsigned* tiles, int ntiles, Live live,
                           int nchains, hipStream_t s,
                           FusedDiag<float> fd = FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0},
@@ -150,7 +151,8 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
 // the far trailing updates of the Newton factorisation on 256x256 quad tiles (chol32.hip): fp16x3
 // operands from the planes only, rows below the appended right-hand side, chains with h3ok set
 void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, int nq, Live live,
-                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl);
+                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl,
+                               int role = 0);
 std::vector<unsigned> build_update_quads(int i0, int R, int j0, int jend);
 // solo >= 0: row tile solo gets super-tile rows of its own (never paired with another row tile)
 std::vector<unsigned> build_update_supertiles(int i0, int R, int j0, int jend, int glo, int ghi,
@@ -286,7 +288,8 @@ void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t v
 // tiles the bottom's updates read included)
 void launch_post32_convert(MatB A, MatF S32, const double* D64, int64_t d64stride, float* D32,
                            int64_t d32stride, int nb, int outer, int k0, int k1, bool bottom,
-                           Live live, int nchains, hipStream_t s);
+                           Live live, int nchains, hipStream_t s,
+                           Planes16 pl = Planes16{nullptr, 0, 0, 0});
 // status[b] = code where other[b] != 0 (chol(K) failure of the concurrent factorisation wins)
 void launch_merge_status(int* status, const int* other, int code, int nchains, hipStream_t s);
 

@@ -142,6 +142,7 @@ struct apm_ctx {
     bool h3 = true;       // APM_H3=0: fp32 operands in the fp32 factorisations' outer updates
     bool h3_now = false;  // some chain of the current theta-call may use fp16x3 updates
     bool h3_all = false;  // ... and every chain may (the quad-tile far updates need that)
+    bool h3post_all = false;  // every chain takes fp16x3 operands in the posterior bottom block
     int* h3ok = nullptr;  // per chain: fp16x3 allowed (range check on theta_0, chol32.hip)
     int* h3post = nullptr;  // the same for the posterior factor's fp32 bottom block (h3ok + B)
     // per chain: explicit-inverse Newton panels allowed (h3ok + 2B): their fp16x3 operands are
@@ -703,8 +704,9 @@ void upload_h3(apm_ctx* c, int count) {
     int* h = pin_h3(c);
     int* v = pin_inv(c);
     c->h3_now = c->inv_any = false;
-    c->h3_all = c->inv_all = count > 0;
+    c->h3_all = c->inv_all = c->h3post_all = count > 0;
     for (int b = 0; b < count; ++b) {
+        c->h3post_all &= pin_h3post(c)[b] != 0;
         v[b] = v[b] && h[b];
         c->h3_now |= h[b] != 0;
         c->h3_all &= h[b] != 0;
@@ -997,6 +999,15 @@ MatF s32_of(apm_ctx* c) {
     return MatF{reinterpret_cast<float*>(c->A.base + c->np), 2 * c->A.ld, 2 * c->A.cstride};
 }
 float* d32post_of(apm_ctx* c) { return reinterpret_cast<float*>(c->Dinv + (int64_t)c->nb * 4096); }
+// fp16x3 operand planes of the bottom block's trailing updates: the Newton planes' memory (free
+// once the Newton loop is done: both parity buffers of a chain hold the 2 np rows of [top;
+// bottom]), written per outer panel by the conversion (the top's rows below the diagonal block)
+// and the bottom rows' walks, read by the quad-tile update on the same stream (stream2), so one
+// buffer serves every panel. Only when every chain of the call takes fp16x3 operands there.
+Planes16 post_planes_of(apm_ctx* c) {
+    if (!c->planes || !c->h3post_all) return Planes16{nullptr, 0, 0, 0};
+    return Planes16{c->planes, 2 * c->plane_cs, c->plane_cs, 2 * c->np};
+}
 
 // one outer panel [K, Kend) of the bottom block on stream s: the rows' walks, then the update of
 // their remaining columns
@@ -1007,18 +1018,25 @@ void post_bottom32_steps(apm_ctx* c, int count, int K, int Kend, hipStream_t s) 
     const int64_t ds32 = 2 * c->dstride;
     const int hlim = c->h3 ? 2 * nb : 0;
     const int row0 = std::max(nb, 2 * nb - Kend);  // rows with a nonzero tile in the panel
+    const Planes16 pl = Kend < nb ? post_planes_of(c) : Planes16{nullptr, 0, 0, 0};
     launch_chol_panel_bulk32(S, K, Kend - K, row0, 2 * nb, 2 * nb,
                              FusedDiag<float>{0, d32post_of(c), ds32, nullptr, 0, 0}, lv, count,
-                             hlim, c->h3post, s);
+                             hlim, c->h3post, s, pl);
     check_launch();
     if (Kend >= nb) return;
-    const auto sl = super_list(c, row0, 2 * nb, Kend, nb, Gap{0, 0});
     const double fl =
         c->prof ? update_flops(row0, 2 * nb, Kend, nb, Kend - K, Gap{0, 0}) * c->live_n : 0.0;
     ProfScope ps(c, APM_PROF_POST32_OUTER, fl, s);
-    launch_chol_update32_t128(S, K, Kend - K, sl.first, sl.second, lv, count, s,
-                              FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, hlim, c->h3post,
-                              -1, /*role: the posterior bottom block*/ 1);
+    if (pl.base) {  // 256x256 quad tiles from the planes (bitwise the split-while-staged kernel)
+        const auto ql = quad_list(c, row0, 2 * nb, Kend, nb);
+        launch_chol_update32_q256(S, K, Kend - K, ql.first, ql.second, lv, count, s, c->h3post,
+                                  pl, /*role: the posterior bottom block*/ 1);
+    } else {
+        const auto sl = super_list(c, row0, 2 * nb, Kend, nb, Gap{0, 0});
+        launch_chol_update32_t128(S, K, Kend - K, sl.first, sl.second, lv, count, s,
+                                  FusedDiag<float>{0, nullptr, 0, nullptr, 0, 0}, hlim, c->h3post,
+                                  -1, /*role: the posterior bottom block*/ 1);
+    }
     check_launch();
 }
 
@@ -1042,7 +1060,8 @@ void post_bottom32_panel(apm_ctx* c, int count, int K, int Kend) {
     HIPC(hipEventRecord(e, c->stream));
     HIPC(hipStreamWaitEvent(c->stream2, e, 0));
     launch_post32_convert(c->A, s32_of(c), c->Dinv, c->dstride, d32post_of(c), 2 * c->dstride,
-                          c->nb, c->outer, K, Kend, false, live_of(c), count, c->stream2);
+                          c->nb, c->outer, K, Kend, false, live_of(c), count, c->stream2,
+                          Kend < c->nb ? post_planes_of(c) : Planes16{nullptr, 0, 0, 0});
     check_launch();
     post_bottom32_steps(c, count, K, Kend, c->stream2);
 }

@@ -492,6 +492,19 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
     const float* Ai = Ab + (int64_t)(i * 64) * A.ld;
     // first column of the walk (BULK with a zero pattern: the row's first nonzero tile column)
     const int kstart = (BULK && zrow > 0) ? max(K, zrow - 1 - i) : K;
+    if (BULK && pl.base && kstart > K && (i + 1) * 64 <= pl.rows) {
+        // the operand planes of the row's known-zero tiles in this panel (the trailing update
+        // reads every panel column of the row)
+        for (int k = K; k < kstart; ++k) {
+            unsigned short* hp = pl.base + b * pl.cstride +
+                                 ((int64_t)(2 * (k - K) + wc) * pl.rows + i * 64 + 32 * wr) * 32;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                hp[64 * q + lane] = 0;
+                hp[pl.lo + 64 * q + lane] = 0;
+            }
+        }
+    }
     for (int k = kstart; k <= last; ++k) {
         const int c = k - kstart;
         DF_STAMP(0);
@@ -633,11 +646,11 @@ __global__ __launch_bounds__(256, BULK ? DF_BULK_WPE : DF_WPE) void k_chol_panel
             DF_STAMP(4);
         } else {
             tile32_store(x, Aik, A.ld, wr, wc, lane);
-            if (!BULK && pl.base && (i + 1) * 64 <= pl.rows) {
+            if (pl.base && (i + 1) * 64 <= pl.rows) {
                 // the trailing update's fp16x3 operand planes: this wave's 32x32 block is rows
                 // 32wr .. +31 of slice 2(k - K) + wc (Planes16)
                 unsigned short* hp = pl.base + b * pl.cstride +
-                                     ((int64_t)(2 * c + wc) * pl.rows + i * 64 + 32 * wr) * 32;
+                                     ((int64_t)(2 * (k - K) + wc) * pl.rows + i * 64 + 32 * wr) * 32;
 #pragma unroll
                 for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -673,12 +686,12 @@ long launch_chol_panel_df32(MatF A, int K, int ncols, int R, FusedDiag<float> fd
 
 void launch_chol_panel_bulk32(MatF A, int K, int ncols, int row0, int R, int zrow,
                               FusedDiag<float> fd, Live live, int nchains, int hlim,
-                              const int* h3ok, hipStream_t s) {
+                              const int* h3ok, hipStream_t s, Planes16 pl) {
     if (ncols < 1 || R <= row0) return;
     APM_LAUNCH(k_chol_panel_df32<true>, dim3((unsigned)((long)(R - row0) * nchains)),
                        dim3(256), 0, s, A, K, ncols, R, nchains, fd, live, hlim, h3ok, nullptr,
-                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0},
-                       Planes16{nullptr, 0, 0, 0}, -1, (const int*)nullptr, row0, zrow);
+                       (int64_t)0, 0ull, SpinCtl{nullptr, 0ull, nullptr, 0}, pl, -1,
+                       (const int*)nullptr, row0, zrow);
 }
 
 // ------------------------------------------------------------------------- 128x128 trailing update
@@ -1118,6 +1131,7 @@ void launch_chol_update32_t128(MatF A, int k0, int kc, const unsigned* tiles, in
 struct __attribute__((aligned(16))) GemmSmemQ {
     _Float16 q[2][4][256][LPH];  // [buffer][A hi, A lo, B hi, B lo][row][k] (HS layout)
 };
+template <int ROLE>  // 0: the Newton factorisation, 1: the posterior bottom block (same code)
 __global__ __launch_bounds__(512, 1) void k_chol_update32_q256(MatF A, int k0, int kc,
                                                                const unsigned* __restrict__ quads,
                                                                int nq, int nchains, Live live,
@@ -1224,10 +1238,15 @@ __global__ __launch_bounds__(512, 1) void k_chol_update32_q256(MatF A, int k0, i
 }
 
 void launch_chol_update32_q256(MatF A, int k0, int kc, const unsigned* quads, int nq, Live live,
-                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl) {
+                               int nchains, hipStream_t s, const int* h3ok, Planes16 pl,
+                               int role) {
     if (nq <= 0 || !pl.base) return;
-    APM_LAUNCH(k_chol_update32_q256, dim3((unsigned)((long)nq * nchains)), dim3(512), 0, s,
-                       A, k0, kc, quads, nq, nchains, live, h3ok, pl);
+    if (role == 1)
+        APM_LAUNCH(k_chol_update32_q256<1>, dim3((unsigned)((long)nq * nchains)), dim3(512), 0,
+                   s, A, k0, kc, quads, nq, nchains, live, h3ok, pl);
+    else
+        APM_LAUNCH(k_chol_update32_q256<0>, dim3((unsigned)((long)nq * nchains)), dim3(512), 0,
+                   s, A, k0, kc, quads, nq, nchains, live, h3ok, pl);
 }
 
 // ------------------------------------------------------------------------- explicit-inverse panel

@@ -258,11 +258,14 @@ void launch_trmv_tiles(bool rev, MatB L, const double* x, double* out, int64_t v
 // [0, T) the top's tiles (i, j), j in [k0, k1), i >= j (rectangular index, upper ones skipped),
 // [T, T + k1 - k0) the diagonal-tile inverses of those columns, then (bottom) the bottom's tiles
 // (I, k), those before the outer panel of the row's first nonzero tile column nb - 1 - I skipped
-// (never read by the bottom's walks and updates).
+// (never read by the bottom's walks and updates). pl.base: the top's tiles below the panel's
+// diagonal block (rows >= k1: the trailing update's column operands) also go to the fp16x3
+// operand planes (Planes16, slice 2 (j - k0) + c / 32), split as the update would split the fp32
+// value (hi = fp16(x), lo = fp16(x - hi)).
 __global__ __launch_bounds__(256) void k_post32_convert(MatB A, MatF S, const double* __restrict__ D64,
                                                         int64_t d64stride, float* __restrict__ D32,
                                                         int64_t d32stride, int nb, int outer,
-                                                        int k0, int k1, Live live) {
+                                                        int k0, int k1, Live live, Planes16 pl) {
     const int b = blockIdx.y;
     if (!live_pc(live, b)) return;
     const int nc = k1 - k0, T = (nb - k0) * nc;
@@ -271,9 +274,12 @@ __global__ __launch_bounds__(256) void k_post32_convert(MatB A, MatF S, const do
     int64_t sld;
     float* dst;
     int64_t dld;
+    unsigned short* hp = nullptr;  // the tile's planes (top tiles below the diagonal block)
     if (t < T) {
         const int ti = k0 + t / nc, tj = k0 + t % nc;
         if (tj > ti) return;
+        if (pl.base && ti >= k1)
+            hp = pl.base + b * pl.cstride + ((int64_t)(2 * (tj - k0)) * pl.rows + ti * 64) * 32;
         src = A.base + b * A.cstride + (int64_t)(ti * 64) * A.ld + tj * 64;
         sld = A.ld;
         dst = S.base + b * S.cstride + (int64_t)(ti * 64) * S.ld + tj * 64;
@@ -297,18 +303,30 @@ __global__ __launch_bounds__(256) void k_post32_convert(MatB A, MatF S, const do
     for (int h = 0; h < 8; ++h) {
         const int e = threadIdx.x + 256 * h, r = e >> 5, c = 2 * (e & 31);
         const d2_t v = *reinterpret_cast<const d2_t*>(src + (int64_t)r * sld + c);
-        *reinterpret_cast<f2_t*>(dst + (int64_t)r * dld + c) = f2_t{(float)v.x, (float)v.y};
+        const f2_t f{(float)v.x, (float)v.y};
+        *reinterpret_cast<f2_t*>(dst + (int64_t)r * dld + c) = f;
+        if (hp) {  // slice 2 (tj - k0) + c / 32, row r, halves c % 32 .. +1
+            const _Float16 h0 = (_Float16)f.x, h1 = (_Float16)f.y;
+            const _Float16 l0 = (_Float16)(f.x - (float)h0), l1 = (_Float16)(f.y - (float)h1);
+            unsigned short* q = hp + ((int64_t)(c >> 5) * pl.rows + r) * 32 + (c & 31);
+            *reinterpret_cast<unsigned*>(q) =
+                __builtin_bit_cast(unsigned short, h0) |
+                ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+            *reinterpret_cast<unsigned*>(q + pl.lo) =
+                __builtin_bit_cast(unsigned short, l0) |
+                ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+        }
     }
 }
 
 void launch_post32_convert(MatB A, MatF S32, const double* D64, int64_t d64stride, float* D32,
                            int64_t d32stride, int nb, int outer, int k0, int k1, bool bottom,
-                           Live live, int nchains, hipStream_t s) {
+                           Live live, int nchains, hipStream_t s, Planes16 pl) {
     const int nc = k1 - k0, T = (nb - k0) * nc;
     const int grid = T + nc + (bottom ? nb * nb : 0);
     if (grid <= 0) return;
     APM_LAUNCH(k_post32_convert, dim3(grid, nchains), dim3(256), 0, s, A, S32, D64,
-                       d64stride, D32, d32stride, nb, outer, k0, k1, live);
+                       d64stride, D32, d32stride, nb, outer, k0, k1, live, pl);
 }
 
 __global__ void k_merge_status(int* status, const int* other, int code, int nchains) {
