@@ -1468,30 +1468,57 @@ __global__ __launch_bounds__(512, 1) void k_panel_inv_gemm32(MatF A, int K, int 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (!mine) return;
-    // X in place (both row tiles were read whole above) and the panel's planes
+    // X in place (both row tiles were read whole above) and the panel's planes, one output
+    // column tile at a time through LDS (the loop ended on a barrier; each wave its own 64 x 68
+    // fp32 region): the accumulators go in by ds_write_b32, then every lane moves 8 consecutive
+    // columns of a row - two 16-byte stores of X, one 16-byte store each of its hi and lo planes
+    // (round 6: the accumulator layout, 4 rows x 1 column per lane and block, went out as 4-byte
+    // stores of X and 2-byte plane stores, 3 scattered stores per element: 4 VALU per MFMA and
+    // the fabric's narrow-store cost in the counters, profiles/r05_pmc_newton_final.txt)
     const int i = i0 + rt;
     float* Ai = Ab + (int64_t)(rt * 64) * A.ld;
     const bool planes = pl.base && (i + 1) * 64 <= pl.rows;
+    constexpr int EP = 68;  // LDS row pitch (floats): 16-byte rows, lane groups 4 rows apart
+                            // on different banks
+    float* ew = reinterpret_cast<float*>(&sm) + wv * (64 * EP);
     auto put = [&](const f4_t (&acc)[4][4], int cc) {
-        unsigned short* hp = planes ? pl.base + b * pl.cstride : nullptr;
+        if (mine) {
 #pragma unroll
-        for (int bi = 0; bi < 4; ++bi)
+            for (int bi = 0; bi < 4; ++bi)
 #pragma unroll
-            for (int bj = 0; bj < 4; ++bj)
+                for (int bj = 0; bj < 4; ++bj)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rr = 16 * bi + F32_CROW(lane, r), col = 64 * cc + 16 * bj + r16;
-                    const float v = acc[bi][bj][r];
-                    Ai[(int64_t)rr * A.ld + col] = v;
-                    if (planes) {
-                        const _Float16 h = (_Float16)v, l = (_Float16)(v - (float)h);
-                        const int64_t o =
-                            ((int64_t)(col >> 5) * pl.rows + i * 64 + rr) * 32 + (col & 31);
-                        hp[o] = __builtin_bit_cast(unsigned short, h);
-                        hp[o + pl.lo] = __builtin_bit_cast(unsigned short, l);
-                    }
+                    for (int r = 0; r < 4; ++r)
+                        ew[(16 * bi + F32_CROW(lane, r)) * EP + 16 * bj + r16] = acc[bi][bj][r];
+        }
+        __syncthreads();
+        if (mine) {
+            // lane: row 8q + (lane >> 3), columns 8 (lane & 7) .. +7 of the tile
+            const int c8 = 8 * (lane & 7), col = 64 * cc + c8;
+            unsigned short* hp =
+                planes ? pl.base + b * pl.cstride + (int64_t)(col >> 5) * pl.rows * 32 + (col & 31)
+                       : nullptr;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int rr = 8 * q + (lane >> 3);
+                const f4_t v0 = *reinterpret_cast<const f4_t*>(ew + rr * EP + c8);
+                const f4_t v1 = *reinterpret_cast<const f4_t*>(ew + rr * EP + c8 + 4);
+                float* dst = Ai + (int64_t)rr * A.ld + col;
+                *reinterpret_cast<f4_t*>(dst) = v0;
+                *reinterpret_cast<f4_t*>(dst + 4) = v1;
+                if (planes) {
+                    h4_t h0, l0, h1, l1;
+                    split_h3(v0, h0, l0);
+                    split_h3(v1, h1, l1);
+                    const h8_t hi = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                    const h8_t lo = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+                    unsigned short* o = hp + (int64_t)(i * 64 + rr) * 32;
+                    *reinterpret_cast<h8_t*>(o) = hi;
+                    *reinterpret_cast<h8_t*>(o + pl.lo) = lo;
                 }
+            }
+        }
+        __syncthreads();  // (the region is rewritten for the second column tile)
     };
     put(acc0, c0);
     put(acc1, c1);
