@@ -1875,7 +1875,8 @@ __global__ __launch_bounds__(256) void k_trsv_bwd32(MatF A, int J, const float* 
 // G - 1 workgroups of a launch can wait on one that has not (role g waits on every role, the
 // round-robin step order has no lower-index-only form), and they wait only until any other
 // workgroup on the GPU retires and frees a slot for it.
-#define TRM_G 4         // workgroups per chain
+#define TRM_G 8         // workgroups per chain
+#define TRM_CHUNK 4     // solution blocks fetched per poll round
 __global__ __launch_bounds__(256) void k_nan_fill(double* out, int64_t vstride, int np,
                                                   Live live) {
     const int b = blockIdx.y;
@@ -1962,12 +1963,17 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
         for (int c = 0; c < 16; ++c) acc[c] = 0.0;
         // all earlier blocks but the previous step's, then that one; the early tiles stream with
         // two tiles' loads in flight ahead of the one being consumed (the step's critical path
-        // is this one workgroup's read of its block row)
+        // is this one workgroup's read of its block row). The solution blocks this workgroup
+        // has not seen yet (the other roles' last steps) are fetched only when the stream reaches
+        // them, so the tiles of the blocks already in LDS are read while those steps finish.
         const int early = s > 0 ? s - 1 : 0;
-        if (have < early) {
-            fetch(have, early);
-            have = early;
-        }
+        auto ensure = [&](int idx) {  // (uniform: `have` is the same in every thread)
+            if (idx < have) return;
+            const int e = early < have + TRM_CHUNK ? early : have + TRM_CHUNK;
+            fetch(have, e);
+            have = e;
+            __syncthreads();
+        };
         __syncthreads();
         {
             f4_t p0[4], p1[4], p2[4];
@@ -1997,14 +2003,23 @@ __global__ __launch_bounds__(256) void k_trsv32_mw(MatF A, int nb, const float* 
             int idx = 0;
             for (; idx + 2 < early; idx += 3) {  // same order of accumulation as one at a time
                 ld4(p2, idx + 2);
+                ensure(idx);
                 use(p0, blk(idx));
                 if (idx + 3 < early) ld4(p0, idx + 3);
+                ensure(idx + 1);
                 use(p1, blk(idx + 1));
                 if (idx + 4 < early) ld4(p1, idx + 4);
+                ensure(idx + 2);
                 use(p2, blk(idx + 2));
             }
-            if (idx < early) use(p0, blk(idx));
-            if (idx + 1 < early) use(p1, blk(idx + 1));
+            if (idx < early) {
+                ensure(idx);
+                use(p0, blk(idx));
+            }
+            if (idx + 1 < early) {
+                ensure(idx + 1);
+                use(p1, blk(idx + 1));
+            }
             if (s > 0) {
                 if (have < s) {
                     fetch(s - 1, s);
