@@ -348,7 +348,11 @@ void launch_guard_check(const double* ldet, int64_t lstride, int nb, const doubl
 // Every launch goes through APM_LAUNCH, which first lets skew_point enqueue a delay kernel on the
 // launch's stream when the calling thread's context asked for it: a cross-stream edge without
 // its wait then reads stale data deterministically instead of by chance.
+#ifdef APM_TOOL_NO_SKEW  // stand-alone development benches that include a .hip file directly
+inline void skew_point(hipStream_t) {}
+#else
 void skew_point(hipStream_t s);
+#endif
 void launch_delay(int us, hipStream_t s);
 #define APM_LAUNCH(kern, grid, block, lds, st, ...)                      \
     do {                                                                 \

@@ -1,5 +1,6 @@
 // Development check of the 64x64 diagonal-tile factorisation (diag.h) against a CPU Cholesky.
 // hipcc --offload-arch=gfx950 -O3 -x hip tools/diag_test.cpp -o tools/diag_test.bin
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol.hip"
 #include <cmath>
 #include <cstdio>

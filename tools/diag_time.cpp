@@ -1,5 +1,6 @@
 // Development timing of the stand-alone diag kernel (64 chains); build with -DDIAG_SKIP=mask to
 // drop phases (1: pivots, 2: 16x16 inverse, 4: panel+trailing, 8: off-diagonal inverse, 16: stores).
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol.hip"
 #include <cstdio>
 #include <vector>

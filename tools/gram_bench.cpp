@@ -2,6 +2,7 @@
 // lower tiles only, K2 copy of the first 8 tile columns) - development tool. Ablations:
 // -DGRAM_ABL=1 no exp, =2 no stores, =3 no distance loop.
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/gram_bench.cpp -o tools/gram.bin
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/gram.hip"
 #include <cstdio>
 #include <cstdlib>

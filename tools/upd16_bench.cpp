@@ -3,6 +3,7 @@
 // (development tool). Ablations:
 // -DH3_ABL=1 every slice reads slice 0 (operands cache-resident), =2 no MFMA.
 // hipcc --offload-arch=gfx950 -O3 -x hip tools/upd16_bench.cpp -o tools/upd16.bin
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol32.hip"
 #include <cstdio>
 #include <cstdlib>

@@ -5,6 +5,7 @@
 // triangle, the bench's roofline accounting) and an output checksum (variants must match it).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/upd32_bench.cpp -o tools/upd32.bin
 //   tools/upd32.bin [chains=64] [K=0] [reps=10]
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol32.hip"
 #include <cstdio>
 #include <cstdlib>

@@ -2,6 +2,7 @@
 // chol(K) shape of N=4096 (development tool). Ablations: -DT64_ABL=1 no MFMA, =2 no operand loads.
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/upd64_bench.cpp \
 //     auxiliary-pm-mcmc_amd/build/chol32.hip.o -o tools/upd64.bin
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol.hip"
 #include <cstdio>
 #include <cstdlib>

@@ -1,5 +1,6 @@
 // Microbenchmark of the f64-MFMA trailing-update kernels on random data (development tool).
 // hipcc --offload-arch=gfx950 -O3 -DUPD_KS=16 -x hip tools/upd_bench.cpp -o tools/upd_ks16.bin
+#define APM_TOOL_NO_SKEW
 #include "../auxiliary-pm-mcmc_amd/csrc/chol.hip"
 #include <cstdio>
 #include <cstdlib>
