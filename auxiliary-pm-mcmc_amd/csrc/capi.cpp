@@ -183,6 +183,9 @@ struct apm_ctx {
     // dataflow launch (one-panel lookahead, chol_range32)
     hipStream_t stream2 = nullptr;
     hipStream_t stream3 = nullptr;
+    // pacing of the concurrent chol(K) (feed_chol_k): panels it may still release in this Newton
+    // iteration, from the previous theta-call's iteration count (newton_last; 0: no pacing)
+    int cholk_quota = 1 << 30, newton_last = 0;
     Edges ev;  // one event per cross-stream edge
     int skew = 0;  // APM_SKEW (tests only): delay kernels in front of launches (skew_point), bit 2
                    // drops the bottom_done wait
@@ -819,6 +822,15 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
     const int64_t rrow = c->np;  // Newton rhs row (extra row block below B)
     int64_t it = 0;
     for (; it < c->max_iters; ++it) {
+        // the concurrent chol(K)'s panels spread over the iterations the previous call took (one
+        // per iteration at the stationary states): released all at once they ran beside the first
+        // two iterations and slowed them more than they gained (-2.5 ms per theta-call)
+        c->cholk_quota = 1 << 30;
+        if (c->newton_last > 0 && c->cholk_next >= 0 && c->cholk_next < c->nb) {
+            const int left = (c->nb - c->cholk_next + c->outer - 1) / c->outer;
+            const int its = std::max<int>(1, c->newton_last - (int)it);
+            c->cholk_quota = (left + its - 1) / its;
+        }
         launch_newton_prep(c->v, c->y, c->n, c->np, lv, count, c->stream);
         check_launch();
         if (mixed) {  // K b and the fp32 B (+ its right-hand side) in one pass over K's lower half
@@ -864,6 +876,8 @@ void newton(apm_ctx* c, int count, std::vector<int>& st_h, bool mixed, int live0
         if (!live) break;
         c->live_n = live;
     }
+    if (mixed) c->newton_last = (int)std::min<int64_t>(it + 1, c->max_iters);
+    c->cholk_quota = 1 << 30;
     bool changed = false;
     for (int b = 0; b < count; ++b)
         if (act[b] != 0 && st_h[b] == 0) {
@@ -927,7 +941,9 @@ MatB bl_of(apm_ctx* c) { return MatB{c->A.base + (int64_t)c->np * c->A.ld, c->A.
 // (ex.s), liveness (active2 / status2, so that Newton convergence does not mask it) and the upper
 // halves of Dinv / ldet (the Newton factorisation uses the lower halves and the top rows of A).
 // chol_k_begin copies K and factors the first outer panel; each feed_chol_k call releases the
-// next outer panel (panel + its trailing update) behind an event of the main stream.
+// next outer panel (panel + its trailing update) behind an event of the main stream, at most
+// cholk_quota per Newton iteration (newton(): the panels left spread over the iterations the
+// previous call took).
 Exec k_exec(apm_ctx* c, hipStream_t s);
 void chol_k_panel(apm_ctx* c, const Exec& ex) {
     const int K = c->cholk_next;
@@ -957,6 +973,8 @@ void chol_k_begin(apm_ctx* c, int count, const Exec& ex, bool copy = true, bool 
 // main stream's TRSVs, whose single-workgroup-per-chain launches leave most CUs idle
 void feed_chol_k(apm_ctx* c) {
     if (c->cholk_next < 0 || c->cholk_next >= c->nb) return;
+    if (c->cholk_quota <= 0) return;
+    --c->cholk_quota;
     hipEvent_t e = c->ev.cholk_rel[c->cholk_next / c->outer];
     HIPC(hipEventRecord(e, c->stream));
     HIPC(hipStreamWaitEvent(c->stream2, e, 0));
