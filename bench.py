@@ -876,15 +876,19 @@ def main():
                           '256x256 quad tiles, the next panel\'s columns on 128x128 super-tiles; '
                           'achieved in fp32-equivalent flops against the fp16 peak / 3)',
                           PEAK_F16X3_TFLOPS,
-                          ('k_chol_update32_q256', 'k_chol_update32_t128<true, 2>',
-                           'k_chol_update32_t128<true, 0>', 'k_chol_update32_t128<false, 0>'),
+                          ('k_chol_update32_q256<0>', 'k_chol_update32_q256',
+                           'k_chol_update32_t128<true, 2>', 'k_chol_update32_t128<true, 0>',
+                           'k_chol_update32_t128<false, 0>'),
                           'f16x3')
     # the posterior factor's fp32 bottom block: the same kernel under its own instantiation name
     # (ROLE = 1, chol32.hip), so its counter figures are its own
-    post32 = mfma_roofline('post32', 'k_chol_update32_t128 on the posterior factor\'s bottom block '
-                           '(L_K J) L\'^-T (fp32 / fp16x3, second stream; postcov.hip)',
+    post32 = mfma_roofline('post32', 'k_chol_update32_q256<1> (fp16x3 operand planes, 256x256 '
+                           'quad tiles; k_chol_update32_t128<*, 1> for batches outside fp16\'s '
+                           'range) on the posterior factor\'s bottom block (L_K J) L\'^-T, second '
+                           'stream; postcov.hip',
                            PEAK_F16X3_TFLOPS,
-                           ('k_chol_update32_t128<true, 1>', 'k_chol_update32_t128<false, 1>'),
+                           ('k_chol_update32_q256<1>', 'k_chol_update32_t128<true, 1>',
+                            'k_chol_update32_t128<false, 1>'),
                            'f16x3')
     # `roofline` is the kernel with the larger share of the step; the other one rides along
     cands = [r for r in (upd64, upd32) if r is not None]
