@@ -342,3 +342,47 @@ def test_guard_residuals_are_rounding_sized(nat, monkeypatch):
     print('worst r1 r2 r3 r4:', worst)
     assert worst[0] <= 1.0 / 20 and worst[1] <= 1e-6 / 20 and worst[2] <= 0.05 / 20, worst
     assert worst[3] <= 1e-4 / 20, worst
+
+
+def test_chol_k_pacing_is_bitwise_neutral(nat):
+    """The concurrent chol(K) releases its panels over the Newton iterations the context's
+    previous theta-call took (capi.cpp newton: cholk_quota), so its schedule depends on what the
+    context did before. A sequence of stationary states (7-8 iterations) -> theta* (fewer: panels
+    left for the drain before the posterior) -> stationary again (paced from the short call) must
+    give, call by call, the bitwise values of a fresh context (no previous call: no pacing)."""
+    import os
+    from gpdemo.utils import synthetic_gp_data
+    B = 16
+    X, y = synthetic_gp_data(4096, 32, 20151009)
+    st = np.load(os.path.join(os.path.dirname(__file__), 'golden',
+                              'stationary_thetas.npy'))[:B].astype(np.float64)
+    star = np.zeros_like(st)
+    star[:, 1:] = 0.5 * np.log(32.0)
+    seq = [st, star, st]
+    idx = np.arange(B)
+
+    def run(ctx, th):
+        out, status, nops = ctx.theta_eval(nat.EST_IS, th, idx, idx)
+        out2, status2 = ctx.u_eval(idx, idx)
+        return out.copy(), out2.copy(), status.copy(), status2.copy(), nops.copy()
+
+    def fresh(th):
+        ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, 256, max_batch=B, n_slots=B, n_ubufs=B)
+        try:
+            ctx.u_normal(idx, np.full(B, 11), idx)
+            return run(ctx, th)
+        finally:
+            ctx.close()
+
+    ctx = nat.Context(X, y, nat.KERNEL_ARD, 1e-8, 256, max_batch=B, n_slots=B, n_ubufs=B)
+    try:
+        ctx.u_normal(idx, np.full(B, 11), idx)
+        got = [run(ctx, th) for th in seq]
+    finally:
+        ctx.close()
+    for c, (g, th) in enumerate(zip(got, seq)):
+        ref = fresh(th)
+        assert (g[2] == 0).all() and (g[3] == 0).all()
+        for a, b, name in zip(g, ref, ('theta-call', 'u-call', 'status', 'u status', 'nops')):
+            np.testing.assert_array_equal(a, b, err_msg='call {0}: {1}'.format(c, name))
+    assert got[1][4].max() < got[0][4].max(), 'theta* should need fewer Newton iterations'
