@@ -39,7 +39,9 @@ static double upd_flops(int i0, int R, int j0, int jend, int kc) {
 int main(int argc, char** argv) {
     const int chains = argc > 1 ? atoi(argv[1]) : 64, K = argc > 2 ? atoi(argv[2]) : 0;
     const int reps = argc > 3 ? atoi(argv[3]) : 10;
-    const int np = 4096, nb = np / 64, outer = 8;
+    // UPD_OUTER: the outer panel width in tiles (8 in the library; 16 measures what 1024-wide
+    // panels would give the trailing update: half the old-tile passes per unit of depth)
+    const int np = 4096, nb = np / 64, outer = getenv("UPD_OUTER") ? atoi(getenv("UPD_OUTER")) : 8;
     const int64_t ld = np, cs = (int64_t)(np + 64) * np;
     float* A;
     hipMalloc(&A, sizeof(float) * cs * chains);
