@@ -1752,8 +1752,18 @@ __global__ __launch_bounds__(256) void k_symv_reduce(const double* __restrict__ 
     const int np = nb * 64;
     if (i >= np) return;
     const double* pb = part + b * pstride + (int64_t)(i >> 6) * nb * 64 + (i & 63);
+    // 16 loads in flight per thread, then added in the same order (a rolled loop waited for
+    // each load in turn)
     double s = 0.0;
-    for (int tj = 0; tj < nb; ++tj) s += pb[(int64_t)tj * 64];
+    int tj = 0;
+    for (; tj + 16 <= nb; tj += 16) {
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = pb[(int64_t)(tj + q) * 64];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s += v[q];
+    }
+    for (; tj < nb; ++tj) s += pb[(int64_t)tj * 64];
     y[b * ystride + i] = s;
     if (Bf.base) {
         float* col = Bf.base + b * Bf.cstride + (int64_t)np * Bf.ld + i;
@@ -2152,6 +2162,7 @@ __global__ __launch_bounds__(256) void k_refine_check(const double* __restrict__
     const int b = blockIdx.x;
     if (!live32(live, b)) return;
     double mx = 0.0, md = 0.0;
+#pragma unroll 4  // (loads of 4 steps in flight)
     for (int i = threadIdx.x; i < np; i += 256) {
         mx = fmax(mx, fabs(x[b * vstride + i]));
         md = fmax(md, fabs(d[b * vstride + i]));

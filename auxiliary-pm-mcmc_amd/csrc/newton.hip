@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void k_newton_check(NewtonVecs v, int n, int n
     const double* fn = v.fnew + b * v.vstride;
     double* f = v.f + b * v.vstride;
     double s = 0.0;
+#pragma unroll 4  // (loads of 4 steps in flight; the sum keeps its order)
     for (int i = threadIdx.x; i < n; i += 256) {
         const double d = fn[i] - f[i];
         s += d * d;
