@@ -372,7 +372,15 @@ __global__ __launch_bounds__(256) void k_lme(const double* __restrict__ partial,
     double mx = -INFINITY;
     for (int s = threadIdx.x; s < S; s += 256) {
         double v = cst;
-        for (int i = 0; i < nb; ++i) v += pb[(int64_t)i * sp + s];
+        int i = 0;
+        for (; i + 16 <= nb; i += 16) {  // 16 loads in flight, added in order
+            double t[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) t[q] = pb[(int64_t)(i + q) * sp + s];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v += t[q];
+        }
+        for (; i < nb; ++i) v += pb[(int64_t)i * sp + s];
         if (s < 1024) lw[s] = v;
         mx = fmax(mx, v);
     }
