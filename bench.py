@@ -978,8 +978,10 @@ def main():
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     cpu, first = None, None
     thetas_par, fix_rows, U1, U2 = parity_inputs(a.n, a.d, a.n_imp)
-    if a.cpu_baseline and dist.rank == 0:
-        try:  # (rank 0 alone: a failure here must not strand the others in the parity check)
+    if a.cpu_baseline and dist.rank == 0 and dist.world == 1:
+        # (N = 1 only, as the bench contract asks; rank 0 alone: a failure here must not strand
+        # the others in the parity check)
+        try:
             cpu, first = cpu_baseline(X, y, a.n_imp, thetas_par[0], n_th, n_u, a.cpu_budget,
                                       U1, U2)
             cpu['gpu_over_cpu_per_chain'] = (value / (a.chains * dist.world)) / cpu['value']
